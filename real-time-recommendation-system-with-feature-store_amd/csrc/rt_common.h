@@ -1,0 +1,107 @@
+// Shared device/host helpers for librtrec_hip.so (gfx950 / CDNA4, wave64).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#include "rtrec_hip.h"
+
+#define RT_WAVE 64
+
+namespace rt {
+
+// thread-local record of the last failing HIP call (rt_last_error)
+void set_last_error(const char* what, hipError_t e);
+
+inline int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        set_last_error(what, e);
+        return RT_ERR_HIP;
+    }
+    return RT_OK;
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- element conversions (widen to f32 on load) ----
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(__half x) { return __half2float(x); }
+__device__ __forceinline__ float to_f32(__hip_bfloat16 x) { return __bfloat162float(x); }
+
+__device__ __forceinline__ float bits_f16_to_f32(uint16_t b) {
+    return __half2float(__ushort_as_half(b));
+}
+__device__ __forceinline__ float bits_bf16_to_f32(uint16_t b) {
+    return __uint_as_float(static_cast<uint32_t>(b) << 16);
+}
+
+// ---- wave reductions (64 lanes) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// ---- counter-based RNG for dropout masks (splitmix64 finaliser) ----
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// keep element (row, col) of a dropout layer with probability 1-p
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, int64_t row, int col, float p) {
+    const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(row) * 0x100000001B3ull + static_cast<uint64_t>(col)));
+    const float u = static_cast<float>(h >> 40) * (1.0f / 16777216.0f);  // [0,1), 24 bits
+    return u >= p;
+}
+
+// ---- activations (src/models/two_tower.py:77-86) ----
+__device__ __forceinline__ float act_fwd(int act, float z) {
+    switch (act) {
+        case RT_ACT_RELU: return z > 0.f ? z : 0.f;
+        case RT_ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+        case RT_ACT_LEAKY_RELU: return z > 0.f ? z : 0.1f * z;
+        case RT_ACT_TANH: return tanhf(z);
+        case RT_ACT_SIGMOID: return 1.f / (1.f + expf(-z));
+        default: return z;
+    }
+}
+// d act / dz evaluated at z
+__device__ __forceinline__ float act_bwd(int act, float z) {
+    switch (act) {
+        case RT_ACT_RELU: return z > 0.f ? 1.f : 0.f;
+        case RT_ACT_GELU: {
+            const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+            const float pdf = 0.39894228040143268f * expf(-0.5f * z * z);
+            return cdf + z * pdf;
+        }
+        case RT_ACT_LEAKY_RELU: return z > 0.f ? 1.f : 0.1f;
+        case RT_ACT_TANH: { const float t = tanhf(z); return 1.f - t * t; }
+        case RT_ACT_SIGMOID: { const float s = 1.f / (1.f + expf(-z)); return s * (1.f - s); }
+        default: return 1.f;
+    }
+}
+
+// ---- (score, id) ordering: a better than b ⇔ score desc, then id asc ----
+// ids are carried as uint32 local indices inside kernels; 0xFFFFFFFF = empty.
+__device__ __forceinline__ bool better(float sa, uint32_t ia, float sb, uint32_t ib) {
+    return sa > sb || (sa == sb && ia < ib);
+}
+
+constexpr uint32_t kEmptyId = 0xFFFFFFFFu;
+
+}  // namespace rt

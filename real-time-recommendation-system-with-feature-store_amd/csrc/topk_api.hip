@@ -1,0 +1,180 @@
+// C ABI for the Flat-IP top-K (rt_flatip_topk) and the candidate-list merge
+// (rt_topk_merge, used for split corpora and for the multi-GPU merge of
+// per-shard top-K lists after an RCCL all-gather).
+#include "topk_impl.h"
+
+namespace rt {
+namespace topk {
+
+// ---- merge [n_lists][nq][k_in] → [nq][k_out], one wave per query ----
+// Candidates stream through a per-wave LDS buffer of N entries: the first
+// k_out slots keep the running best, the rest take new candidates, then sort.
+// ids are carried as uint32 (0 <= id < 2^32-1).
+constexpr int kMergeN = 1024;
+
+__global__ __launch_bounds__(256) void topk_merge_kernel(const float* __restrict__ s_in,
+                                                         const int64_t* __restrict__ i_in, int64_t nq,
+                                                         int n_lists, int k_in, int k_out,
+                                                         float* __restrict__ s_out,
+                                                         int64_t* __restrict__ i_out) {
+    __shared__ Cand buf[4][kMergeN];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + w;
+    if (q >= nq) return;
+    Cand* b = buf[w];
+    const int64_t total = static_cast<int64_t>(n_lists) * k_in;
+    int want = total < kMergeN ? static_cast<int>(total) : kMergeN;
+    if (want < k_out + 64) want = k_out + 64;  // room for new candidates each round
+    int n = next_pow2(want);
+    if (n > kMergeN) n = kMergeN;
+    int kept = 0;
+    int64_t next = 0;
+    for (;;) {
+        for (int e = kept + lane; e < n; e += 64) {
+            const int64_t src = next + (e - kept);
+            Cand c{-INFINITY, kEmptyId};
+            if (src < total) {
+                const int l = static_cast<int>(src / k_in);
+                const int j = static_cast<int>(src - static_cast<int64_t>(l) * k_in);
+                const int64_t off = (static_cast<int64_t>(l) * nq + q) * k_in + j;
+                const int64_t id = i_in[off];
+                if (id >= 0) c = Cand{s_in[off], static_cast<uint32_t>(id)};
+            }
+            b[e] = c;
+        }
+        next += n - kept;
+        wave_lds_sync();
+        wave_sort_lds(b, n);
+        kept = k_out;
+        if (next >= total) break;
+    }
+    for (int e = lane; e < k_out; e += 64) {
+        const Cand c = b[e];
+        const bool ok = c.i != kEmptyId;
+        s_out[q * k_out + e] = ok ? c.s : -FLT_MAX;
+        i_out[q * k_out + e] = ok ? static_cast<int64_t>(c.i) : -1;
+    }
+}
+
+int launch_merge(const float* s, const int64_t* ids, int64_t nq, int n_lists, int k_in, int k_out,
+                 float* os, int64_t* oi, hipStream_t st) {
+    if (k_out + 64 > kMergeN) return RT_ERR_UNSUPPORTED;
+    dim3 grid(static_cast<unsigned>((nq + 3) / 4));
+    hipLaunchKernelGGL(topk_merge_kernel, grid, dim3(256), 0, st, s, ids, nq, n_lists, k_in, k_out, os, oi);
+    return check_launch("topk_merge_kernel");
+}
+
+inline int cap_for(int k) {
+    int c = 128;
+    while (c < k + kNT) c <<= 1;
+    return c;
+}
+
+inline Plan make_plan(int64_t nq, int64_t nx, int k) {
+    Plan p{};
+    p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
+    if (p.chunk < 1) p.chunk = 1;
+    p.q_tiles = static_cast<int>((p.chunk + kQT - 1) / kQT);
+    // enough blocks to fill 256 CUs ~2x, but keep >= 4 item tiles per split
+    const int64_t tiles = (nx + kNT - 1) / kNT;
+    int64_t splits = (512 + p.q_tiles - 1) / p.q_tiles;
+    int64_t max_splits = tiles / 4;
+    if (max_splits < 1) max_splits = 1;
+    if (splits > max_splits) splits = max_splits;
+    if (splits > 64) splits = 64;
+    if (splits < 1) splits = 1;
+    int64_t tiles_per = (tiles + splits - 1) / splits;
+    if (tiles_per < 1) tiles_per = 1;
+    p.items_per_split = tiles_per * kNT;
+    p.splits = static_cast<int>(nx > 0 ? (nx + p.items_per_split - 1) / p.items_per_split : 1);
+    p.cap = cap_for(k);
+    p.cand_bytes = static_cast<size_t>(p.splits) * p.q_tiles * kQT * p.cap * sizeof(Cand);
+    p.part_bytes = p.splits > 1 ? static_cast<size_t>(p.splits) * p.chunk * k * (sizeof(float) + sizeof(int64_t)) : 0;
+    return p;
+}
+
+inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+
+}  // namespace topk
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" size_t rt_flatip_topk_workspace_bytes(int64_t nq, int64_t nx, int d, int dtype, int k) {
+    (void)d;
+    (void)dtype;
+    if (nq <= 0 || k <= 0 || k > topk::kMaxK) return 256;
+    const topk::Plan p = topk::make_plan(nq, nx, k);
+    return topk::align256(p.cand_bytes) + p.part_bytes + 256;
+}
+
+extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
+                              int dtype, int k, const uint32_t* exclude_bits, int64_t exclude_words,
+                              int64_t id_offset, float* out_scores, int64_t* out_ids, void* workspace,
+                              size_t workspace_bytes, void* stream) {
+    if (nq < 0 || nx < 0 || d <= 0 || k <= 0) return RT_ERR_INVALID;
+    if (nq == 0) return RT_OK;
+    if (!queries || !out_scores || !out_ids || (nx > 0 && !items)) return RT_ERR_INVALID;
+    if (k > topk::kMaxK) return RT_ERR_UNSUPPORTED;
+    if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return RT_ERR_INVALID;
+    if (dtype == RT_F32 ? (d % 4 != 0 || d > 128) : (d % 8 != 0 || d > 256)) return RT_ERR_UNSUPPORTED;
+    if (nx >= 0xFFFFFFFFll || (id_offset + nx) >= 0xFFFFFFFFll || id_offset < 0) return RT_ERR_UNSUPPORTED;
+    if ((reinterpret_cast<uintptr_t>(queries) | reinterpret_cast<uintptr_t>(items)) & 15) return RT_ERR_INVALID;
+    if (exclude_bits && exclude_words < (nx + 31) / 32) return RT_ERR_INVALID;
+    const topk::Plan p = topk::make_plan(nq, nx, k);
+    const size_t cand_al = topk::align256(p.cand_bytes);
+    if (!workspace || workspace_bytes < cand_al + p.part_bytes) return RT_ERR_WORKSPACE;
+    hipStream_t st = as_stream(stream);
+    char* part = reinterpret_cast<char*>(workspace) + cand_al;
+    const size_t esz = dtype == RT_F32 ? 4 : 2;
+    for (int64_t q0 = 0; q0 < nq; q0 += p.chunk) {
+        const int64_t nc = (nq - q0) < p.chunk ? (nq - q0) : p.chunk;
+        float* os = out_scores + q0 * k;
+        int64_t* oi = out_ids + q0 * k;
+        int rc;
+        if (nx == 0) {  // empty corpus: every slot (-FLT_MAX, -1)
+            rc = topk::launch_merge(os, oi, nc, 0, 1, k, os, oi, st);
+            if (rc) return rc;
+            continue;
+        }
+        topk::Args a{};
+        a.Q = reinterpret_cast<const char*>(queries) + q0 * d * esz;
+        a.nq = nc;
+        a.X = items;
+        a.nx = nx;
+        a.d = d;
+        a.k = k;
+        a.excl = exclude_bits ? exclude_bits + q0 * exclude_words : nullptr;
+        a.excl_words = exclude_words;
+        a.cand = reinterpret_cast<Cand*>(workspace);
+        a.id_offset = id_offset;
+        if (p.splits > 1) {  // per-split lists [split][nc][k], merged below
+            a.out_s = reinterpret_cast<float*>(part);
+            a.out_i = reinterpret_cast<int64_t*>(part + static_cast<size_t>(p.splits) * p.chunk * k * sizeof(float));
+        } else {
+            a.out_s = os;
+            a.out_i = oi;
+        }
+        switch (dtype) {
+            case RT_F32: rc = topk::launch_f32(a, p, st); break;
+            case RT_F16: rc = topk::launch_f16(a, p, st); break;
+            default: rc = topk::launch_bf16(a, p, st); break;
+        }
+        if (rc) return rc;
+        if (p.splits > 1) {
+            rc = topk::launch_merge(a.out_s, a.out_i, nc, p.splits, k, k, os, oi, st);
+            if (rc) return rc;
+        }
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int n_lists, int k_in,
+                             int k_out, float* out_scores, int64_t* out_ids, void* stream) {
+    if (nq < 0 || n_lists < 0 || k_in <= 0 || k_out <= 0) return RT_ERR_INVALID;
+    if (nq == 0) return RT_OK;
+    if (!out_scores || !out_ids || (n_lists > 0 && (!scores || !ids))) return RT_ERR_INVALID;
+    if (k_out > topk::kMaxK) return RT_ERR_UNSUPPORTED;
+    return topk::launch_merge(scores, ids, nq, n_lists, k_in, k_out, out_scores, out_ids, as_stream(stream));
+}

@@ -1,0 +1,150 @@
+"""Torch-facing wrappers of the HIP C ABI (include/rtrec_hip.h).
+
+Every function here launches hand-written gfx950 kernels from
+librtrec_hip.so on torch's current stream; none has a CPU path (CPU tensors
+raise). Shapes/dtypes are validated on the host before any launch so a bad
+call never reaches the GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import native
+from .native import call, ptr, stream_of
+
+# ---------------------------------------------------------------------------
+# workspace cache (grow-only, per device): no allocation inside hot calls
+# ---------------------------------------------------------------------------
+_WS = {}
+
+
+def workspace(device: torch.device, nbytes: int, tag: str = "ws") -> torch.Tensor:
+    key = (device.index if device.index is not None else torch.cuda.current_device(), tag)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+# ---------------------------------------------------------------------------
+# row gather (src/training/datasets/movielens.py:108-116; nn.Embedding lookup)
+# ---------------------------------------------------------------------------
+
+def gather_rows(table: torch.Tensor, ids: torch.Tensor, row_begin: int = 0,
+                out: Optional[torch.Tensor] = None, oob: Optional[torch.Tensor] = None,
+                check: bool = False) -> torch.Tensor:
+    """``out[r] = table[ids[r] - row_begin]``; ids outside the table give zero rows
+    (counted in ``oob`` if given). ``check=True`` raises IndexError on any
+    out-of-range id like numpy fancy indexing (costs a device sync)."""
+    native.require_device(table, ids, what="gather_rows")
+    if ids.dtype != torch.int64:
+        ids = ids.to(torch.int64)
+    ids = ids.contiguous()
+    table = table.contiguous()
+    row_shape = table.shape[1:]
+    row_bytes = table[0].numel() * table.element_size() if table.shape[0] > 0 else \
+        int(torch.tensor(row_shape).prod()) * table.element_size()
+    if out is None:
+        out = torch.empty((ids.numel(),) + tuple(row_shape), dtype=table.dtype, device=table.device)
+    if check and oob is None:
+        oob = torch.zeros(1, dtype=torch.int32, device=table.device)
+    call("rt_gather_rows", ptr(table), row_begin, table.shape[0], row_bytes, ptr(ids), ids.numel(),
+         ptr(out), ptr(oob), stream_of(table))
+    if check and int(oob.item()) != 0:
+        raise IndexError(f"{int(oob.item())} ids out of range for table of {table.shape[0]} rows")
+    return out.view(tuple(ids.shape) + tuple(row_shape))
+
+
+def scatter_add_rows(grad_table: torch.Tensor, ids: torch.Tensor, grad_out: torch.Tensor,
+                     padding_idx: int = -1) -> torch.Tensor:
+    """nn.Embedding backward: grad_table[ids[r]] += grad_out[r] (padding_idx skipped)."""
+    native.require_device(grad_table, ids, grad_out, what="scatter_add_rows")
+    ids = ids.contiguous().to(torch.int64)
+    grad_out = grad_out.contiguous().float()
+    call("rt_scatter_add_rows_f32", ptr(grad_table), grad_table.shape[0], grad_table.shape[1], ptr(ids),
+         ids.numel(), ptr(grad_out), padding_idx, stream_of(grad_table))
+    return grad_table
+
+
+# ---------------------------------------------------------------------------
+# Faiss normalize_L2 + IndexFlatIP search (src/serving/retrieval.py:86,167,171)
+# ---------------------------------------------------------------------------
+
+def l2_renorm_(x: torch.Tensor) -> torch.Tensor:
+    """In-place ``faiss.normalize_L2`` on fp32 rows."""
+    native.require_device(x, what="l2_renorm_")
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 2:
+        raise ValueError("l2_renorm_ expects a contiguous fp32 [n, d] tensor")
+    call("rt_l2_renorm_f32", ptr(x), x.shape[0], x.shape[1], stream_of(x))
+    return x
+
+
+def flatip_topk(queries: torch.Tensor, items: torch.Tensor, k: int,
+                exclude_bits: Optional[torch.Tensor] = None, id_offset: int = 0,
+                out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact inner-product top-k: (scores [nq,k] f32, ids [nq,k] int64), ordered by
+    (score desc, id asc); unfilled slots are (-FLT_MAX, -1)."""
+    native.require_device(queries, items, what="flatip_topk")
+    if queries.dim() != 2 or items.dim() != 2 or queries.shape[1] != items.shape[1]:
+        raise ValueError(f"shape mismatch: queries {tuple(queries.shape)} items {tuple(items.shape)}")
+    if queries.dtype != items.dtype:
+        raise TypeError("queries and items must share a dtype")
+    if k <= 0:
+        raise ValueError("k must be positive")
+    queries = queries.contiguous()
+    items = items.contiguous()
+    nq, d = queries.shape
+    nx = items.shape[0]
+    dt = native.dtype_code(queries.dtype)
+    if out is None:
+        scores = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
+        ids = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+    else:
+        scores, ids = out
+    if nq == 0:
+        return scores, ids
+    words = 0
+    if exclude_bits is not None:
+        exclude_bits = exclude_bits.contiguous()
+        if exclude_bits.dtype not in (torch.int32, torch.uint32) or exclude_bits.shape[0] != nq:
+            raise ValueError("exclude_bits must be int32/uint32 [nq, words]")
+        words = exclude_bits.shape[1]
+    nbytes = native.lib().rt_flatip_topk_workspace_bytes(nq, nx, d, dt, k)
+    ws = workspace(queries.device, nbytes, "topk")
+    call("rt_flatip_topk", ptr(queries), nq, ptr(items) if nx else None, nx, d, dt, k, ptr(exclude_bits),
+         words, id_offset, ptr(scores), ptr(ids), ptr(ws), ws.numel(), stream_of(queries))
+    return scores, ids
+
+
+def topk_merge(scores: torch.Tensor, ids: torch.Tensor, k_out: int
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Merge candidate lists [n_lists, nq, k_in] into the (score desc, id asc) top k_out."""
+    native.require_device(scores, ids, what="topk_merge")
+    scores = scores.contiguous().float()
+    ids = ids.contiguous().to(torch.int64)
+    n_lists, nq, k_in = scores.shape
+    os_ = torch.empty((nq, k_out), dtype=torch.float32, device=scores.device)
+    oi = torch.empty((nq, k_out), dtype=torch.int64, device=scores.device)
+    call("rt_topk_merge", ptr(scores), ptr(ids), nq, n_lists, k_in, k_out, ptr(os_), ptr(oi),
+         stream_of(scores))
+    return os_, oi
+
+
+def exclusion_bitmap(n_queries: int, n_items: int, excluded, device) -> torch.Tensor:
+    """int32 bitmap [nq, ceil(n_items/32)] (bit j of row q set ⇒ item j skipped for
+    query q) from per-query excluded item lists — the train-item mask of
+    scripts/evaluate_model.py:225-228. Host-side construction."""
+    import numpy as np
+    words = (n_items + 31) // 32
+    mask = np.zeros((n_queries, words * 32), dtype=bool)
+    for q, items in enumerate(excluded):
+        sel = [int(i) for i in items if 0 <= int(i) < n_items]
+        if sel:
+            mask[q, sel] = True
+    packed = np.packbits(mask, axis=1, bitorder="little")  # little-endian words: bit j = item j
+    return torch.from_numpy(np.ascontiguousarray(packed).view(np.int32).copy()).to(device)

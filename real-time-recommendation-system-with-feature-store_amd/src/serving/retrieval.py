@@ -1,0 +1,381 @@
+"""Retrieval layer: the reference's ``IndexBase`` / ``RetrievalEngine`` surface
+(src/serving/retrieval.py:16-46, 505-692) over an MI355X-resident exact
+inner-product index.
+
+``HipFlatIPIndex`` is the drop-in for ``FaissIndex`` in ``Flat`` mode
+(retrieval.py:49-329): same constructor config keys, same
+``build/search/add/save/load`` behaviour and errors, same ``(ids, scores)``
+result lists, but the corpus lives in HBM and ``search`` runs the gfx950
+Flat-IP top-K kernel (MFMA scoring + wavefront select) instead of Faiss-CPU.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import pickle
+import struct
+import time
+from abc import ABC, abstractmethod
+from pathlib import Path
+from typing import Any, Dict, List, Optional, Tuple, Union
+
+import numpy as np
+import torch
+
+from .. import kernels
+
+Array = Union[np.ndarray, torch.Tensor]
+
+
+class _Log:
+    """Tiny stand-in for the reference's loguru calls (loguru is not a dependency)."""
+
+    def __init__(self):
+        import logging
+        self._l = logging.getLogger("rtrec_amd.retrieval")
+
+    def info(self, *a):
+        self._l.info(*a)
+
+    def warning(self, *a):
+        self._l.warning(*a)
+
+    def debug(self, *a):
+        self._l.debug(*a)
+
+
+logger = _Log()
+
+
+class IndexBase(ABC):
+    """Abstract base class for ANN indices (retrieval.py:16-46)."""
+
+    @abstractmethod
+    def build(self, embeddings: np.ndarray, ids: List[str]):
+        """Build the index from embeddings."""
+
+    @abstractmethod
+    def search(self, query_embeddings: np.ndarray, k: int = 10) -> Tuple[np.ndarray, np.ndarray]:
+        """Search for nearest neighbors."""
+
+    @abstractmethod
+    def add(self, embeddings: np.ndarray, ids: List[str]):
+        """Add new embeddings to the index."""
+
+    @abstractmethod
+    def save(self, path: str):
+        """Save index to disk."""
+
+    @abstractmethod
+    def load(self, path: str):
+        """Load index from disk."""
+
+
+_STORAGE = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
+
+
+def _default_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("HipFlatIPIndex needs a ROCm device (no CPU fallback in the MI355X build)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class HipFlatIPIndex(IndexBase):
+    """Exact inner-product index resident in HBM (FaissIndex ``Flat`` semantics).
+
+    Config keys (retrieval.py:58-63): ``dimension`` (128), ``metric``
+    ("cosine" → normalize_L2 on build/add/search, else raw inner product),
+    ``index_factory`` (only recorded: every factory is served exactly),
+    ``nprobe`` (ignored, exact), plus ``device`` and ``storage_dtype``
+    ("float32" default = Faiss numerics; "float16"/"bfloat16" halve the bytes).
+    """
+
+    def __init__(self, config: Optional[Dict[str, Any]] = None):
+        self.config = config or {}
+        self.dimension = self.config.get("dimension", 128)
+        self.index_factory = self.config.get("index_factory", "Flat")
+        self.metric = self.config.get("metric", "cosine")
+        self.nprobe = self.config.get("nprobe", 20)
+        self.storage_dtype = _STORAGE[self.config.get("storage_dtype", "float32")]
+        dev = self.config.get("device")
+        self.device = torch.device(dev) if dev is not None else None
+        self.index: Optional[torch.Tensor] = None   # [capacity, d] device rows; first current_size valid
+        self.id_map: Dict[int, str] = {}
+        self.reverse_id_map: Dict[str, int] = {}
+        self._ids: List[str] = []                  # position -> id (vectorised id_map)
+        self.current_size = 0
+        if "IVF" in str(self.index_factory):
+            logger.warning("index_factory %s: the MI355X index serves every factory exactly (Flat)",
+                           self.index_factory)
+
+    # -- helpers -----------------------------------------------------------
+    def _dev(self) -> torch.device:
+        if self.device is None:
+            self.device = _default_device()
+        return self.device
+
+    def _prepare(self, x: Array) -> torch.Tensor:
+        """Copy to a contiguous fp32 device tensor (the index owns its vectors,
+        retrieval.py:82) and renormalise in place for the cosine metric."""
+        t = torch.as_tensor(x) if not isinstance(x, torch.Tensor) else x
+        if t.dim() == 1:
+            t = t.reshape(1, -1)
+        t = t.to(device=self._dev(), dtype=torch.float32, copy=True).contiguous()
+        if t.shape[1] != self.dimension:
+            raise ValueError(f"expected dimension {self.dimension}, got {t.shape[1]}")
+        if self.metric == "cosine":
+            kernels.l2_renorm_(t)
+        return t
+
+    def _store(self, rows: torch.Tensor):
+        rows = rows.to(self.storage_dtype)
+        n_new = self.current_size + rows.shape[0]
+        if self.index is None or self.index.shape[0] < n_new:
+            cap = max(n_new, 2 * (self.index.shape[0] if self.index is not None else 0), 1024)
+            buf = torch.empty((cap, self.dimension), dtype=self.storage_dtype, device=self._dev())
+            if self.index is not None and self.current_size:
+                buf[: self.current_size].copy_(self.index[: self.current_size])
+            self.index = buf
+        self.index[self.current_size:n_new].copy_(rows)
+
+    # -- IndexBase ---------------------------------------------------------
+    def build(self, embeddings: Array, ids: List[str]):
+        """retrieval.py:70-139 (Flat path)."""
+        start = time.time()
+        rows = self._prepare(embeddings)
+        self.index = None
+        self.current_size = 0
+        self.id_map, self.reverse_id_map, self._ids = {}, {}, []
+        self._store(rows)
+        for i, item_id in enumerate(ids):
+            self.id_map[i] = item_id
+            self.reverse_id_map[item_id] = i
+        self._ids = list(ids) + [None] * max(0, rows.shape[0] - len(ids))
+        self.current_size = rows.shape[0]
+        logger.info("Index built in %.2f seconds", time.time() - start)
+
+    def search_tensors(self, query_embeddings: Array, k: int,
+                       exclude_bits: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Device-level search: (scores [nq,k], positions [nq,k]) with -1 padding."""
+        if self.index is None:
+            raise ValueError("Index not built yet")
+        q = self._prepare(query_embeddings).to(self.storage_dtype)
+        return kernels.flatip_topk(q, self.index[: self.current_size], k, exclude_bits=exclude_bits)
+
+    def search(self, query_embeddings: Array, k: int = 10,
+               filter_ids: Optional[List[str]] = None) -> Tuple[List[List[str]], List[List[float]]]:
+        """retrieval.py:141-197: normalise, top-k_search (2k when filtering), map
+        positions to ids, drop -1 padding, apply the filter, stop at k."""
+        if self.index is None:
+            raise ValueError("Index not built yet")
+        k_search = min(k * 2, self.current_size) if filter_ids else k
+        if k_search <= 0:
+            n = 1 if np.ndim(query_embeddings) == 1 else len(query_embeddings)
+            return [[] for _ in range(n)], [[] for _ in range(n)]
+        scores, pos = self.search_tensors(query_embeddings, k_search)
+        scores = scores.cpu().numpy()
+        pos = pos.cpu().numpy()
+        allowed = set(filter_ids) if filter_ids is not None else None
+        batch_ids, batch_scores = [], []
+        for i in range(pos.shape[0]):
+            item_ids, item_scores = [], []
+            for j in range(k_search):
+                p = int(pos[i, j])
+                if p >= 0 and p in self.id_map:
+                    item_id = self.id_map[p]
+                    if allowed is None or item_id in allowed:
+                        item_ids.append(item_id)
+                        item_scores.append(float(scores[i, j]))
+                        if len(item_ids) >= k:
+                            break
+            batch_ids.append(item_ids)
+            batch_scores.append(item_scores)
+        return batch_ids, batch_scores
+
+    def add(self, embeddings: Array, ids: List[str]):
+        """retrieval.py:199-226: incremental append (Kafka item_update path)."""
+        if self.index is None:
+            raise ValueError("Index not built yet")
+        rows = self._prepare(embeddings)
+        self._store(rows)
+        for i, item_id in enumerate(ids):
+            new_idx = self.current_size + i
+            self.id_map[new_idx] = item_id
+            self.reverse_id_map[item_id] = new_idx
+        self._ids.extend(list(ids) + [None] * max(0, rows.shape[0] - len(ids)))
+        self.current_size += rows.shape[0]
+        logger.info("Added %d items to index. Total size: %d", rows.shape[0], self.current_size)
+
+    def update(self, embeddings: Array, ids: List[str]):
+        """retrieval.py:228-237 (no-op with a warning, like the reference)."""
+        logger.warning("Flat index doesn't support direct updates. Consider periodic rebuilds.")
+
+    def remove(self, ids: List[str]):
+        logger.warning("Flat index doesn't support removal. Consider periodic rebuilds.")
+
+    def vectors(self) -> np.ndarray:
+        if self.index is None:
+            return np.zeros((0, self.dimension), np.float32)
+        return self.index[: self.current_size].float().cpu().numpy()
+
+    def save(self, path: str):
+        """retrieval.py:248-273: ``<path>.faiss`` (IndexFlatIP/IndexFlatL2 binary
+        layout: fourcc, header, code vector) + ``<path>.pkl`` id maps."""
+        if self.index is None:
+            raise ValueError("No index to save")
+        path = Path(path)
+        path.parent.mkdir(parents=True, exist_ok=True)
+        write_flat_index(path.with_suffix(".faiss"), self.vectors(), self.metric == "cosine" or self.metric == "ip")
+        with open(path.with_suffix(".pkl"), "wb") as f:
+            pickle.dump({"id_map": self.id_map, "reverse_id_map": self.reverse_id_map,
+                         "current_size": self.current_size, "config": self.config}, f)
+        logger.info("Saved index to %s", path)
+
+    def load(self, path: str):
+        """retrieval.py:275-299."""
+        path = Path(path)
+        vecs, _ip = read_flat_index(path.with_suffix(".faiss"))
+        with open(path.with_suffix(".pkl"), "rb") as f:
+            data = pickle.load(f)  # files this index wrote (same layout as the reference's)
+        self.id_map = data["id_map"]
+        self.reverse_id_map = data["reverse_id_map"]
+        self.config = data.get("config", self.config)
+        self.dimension = vecs.shape[1]
+        self.index = None
+        self.current_size = 0
+        self._store(torch.from_numpy(vecs).to(self._dev()))
+        self.current_size = int(data["current_size"])
+        self._ids = [self.id_map.get(i) for i in range(self.current_size)]
+        logger.info("Loaded index from %s with %d items", path, self.current_size)
+
+
+# Faiss 1.7.x binary layout of IndexFlat (restated from the published format:
+# fourcc, d:int32, ntotal:int64, 2 x dummy int64, is_trained:bool, metric:int32,
+# then the code vector as a size_t count of floats followed by the floats).
+_FOURCC_IP = b"IxFI"
+_FOURCC_L2 = b"IxF2"
+
+
+def write_flat_index(path: Path, vecs: np.ndarray, inner_product: bool = True):
+    vecs = np.ascontiguousarray(vecs, dtype=np.float32)
+    n, d = vecs.shape
+    with open(path, "wb") as f:
+        f.write(_FOURCC_IP if inner_product else _FOURCC_L2)
+        f.write(struct.pack("<iqqq?i", d, n, 1 << 20, 1 << 20, True, 0 if inner_product else 1))
+        f.write(struct.pack("<Q", n * d))
+        f.write(vecs.tobytes())
+
+
+def read_flat_index(path: Path) -> Tuple[np.ndarray, bool]:
+    with open(path, "rb") as f:
+        four = f.read(4)
+        if four not in (_FOURCC_IP, _FOURCC_L2):
+            raise ValueError(f"{path}: not a flat index (fourcc {four!r})")
+        d, n, _, _, _, _metric = struct.unpack("<iqqq?i", f.read(struct.calcsize("<iqqq?i")))
+        (cnt,) = struct.unpack("<Q", f.read(8))
+        if cnt != n * d:
+            raise ValueError(f"{path}: corrupt code vector ({cnt} != {n}*{d})")
+        vecs = np.frombuffer(f.read(cnt * 4), dtype=np.float32).reshape(n, d).copy()
+    return vecs, four == _FOURCC_IP
+
+
+# Backwards-compatible name: configs with index_type "faiss" get the exact
+# HBM-resident index (Faiss-CPU is not part of the MI355X build).
+FaissIndex = HipFlatIPIndex
+
+_INDEX_TYPES = {"hip_flat": HipFlatIPIndex, "faiss": HipFlatIPIndex}
+
+
+def register_index(name: str, cls):
+    """Plugin hook: make ``RetrievalEngine(config)`` accept ``index_type=name``."""
+    _INDEX_TYPES[name] = cls
+
+
+class RetrievalEngine:
+    """High-level retrieval engine with md5 query cache and metrics
+    (retrieval.py:505-692)."""
+
+    def __init__(self, config: Dict[str, Any]):
+        self.config = config
+        self.index_type = config.get("index_type", "faiss")
+        self.top_k = config.get("top_k", 100)
+        self.update_interval = config.get("update_interval_seconds", 300)
+        self.index = self._create_index()
+        self.cache: Dict[str, Dict[str, Any]] = {}
+        self.cache_ttl = config.get("cache_ttl", 300)
+        self.last_cache_clear = time.time()
+        self.total_queries = 0
+        self.cache_hits = 0
+        self.total_latency = 0.0
+
+    def _create_index(self) -> IndexBase:
+        """retrieval.py:532-544 string dispatch (+ the "hip_flat" type)."""
+        index_config = dict(self.config.get(self.index_type, {}) or {})
+        index_config["dimension"] = self.config.get("embedding_dim", 128)
+        cls = _INDEX_TYPES.get(self.index_type)
+        if cls is None:
+            raise ValueError(f"Unknown index type: {self.index_type}")
+        return cls(index_config)
+
+    def build_index(self, embeddings: Array, ids: List[str]):
+        self.index.build(embeddings, ids)
+        self.cache.clear()
+        logger.info("Built index with %d items", len(embeddings))
+
+    def retrieve(self, query_embeddings: Array, k: Optional[int] = None,
+                 filter_ids: Optional[List[str]] = None, use_cache: bool = True
+                 ) -> Tuple[List[List[str]], List[List[float]], Dict[str, Any]]:
+        start = time.time()
+        k = k or self.top_k
+        cache_key = None
+        if use_cache and filter_ids is None:
+            qb = query_embeddings.detach().cpu().numpy().tobytes() if isinstance(query_embeddings, torch.Tensor) \
+                else np.asarray(query_embeddings).tobytes()
+            cache_key = hashlib.md5(qb).hexdigest()
+            entry = self.cache.get(cache_key)
+            if entry is not None and time.time() - entry["timestamp"] < self.cache_ttl:
+                self.cache_hits += 1
+                latency = time.time() - start
+                self.total_queries += 1
+                self.total_latency += latency
+                return entry["ids"], entry["scores"], {"latency_ms": latency * 1000, "cache_hit": True}
+        item_ids, scores = self.index.search(query_embeddings, k, filter_ids)
+        if use_cache and cache_key:
+            self.cache[cache_key] = {"ids": item_ids, "scores": scores, "timestamp": time.time()}
+            if time.time() - self.last_cache_clear > self.cache_ttl:
+                self._clear_expired_cache()
+        latency = time.time() - start
+        self.total_queries += 1
+        self.total_latency += latency
+        flat = [s for sl in scores for s in sl]
+        metrics = {"latency_ms": latency * 1000, "cache_hit": False,
+                   "num_results": sum(len(x) for x in item_ids),
+                   "avg_score": float(np.mean(flat)) if flat else float("nan")}
+        return item_ids, scores, metrics
+
+    def update_index(self, new_embeddings: Array, new_ids: List[str]):
+        self.index.add(new_embeddings, new_ids)
+        self.cache.clear()
+
+    def _clear_expired_cache(self):
+        now = time.time()
+        for key in [k for k, e in self.cache.items() if now - e["timestamp"] > self.cache_ttl]:
+            del self.cache[key]
+        self.last_cache_clear = now
+
+    def get_metrics(self) -> Dict[str, Any]:
+        return {
+            "total_queries": self.total_queries,
+            "avg_latency_ms": self.total_latency / max(self.total_queries, 1) * 1000,
+            "cache_hit_rate": self.cache_hits / max(self.total_queries, 1),
+            "cache_size": len(self.cache),
+            "index_size": self.index.current_size,
+            "index_type": self.index_type,
+        }
+
+    def save(self, path: str):
+        self.index.save(path)
+
+    def load(self, path: str):
+        self.index.load(path)
+        self.cache.clear()
