@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Benchmark: user-item pairs scored/sec (train) + top-K queries/sec, emb_dim=128.
+
+Headline (BASELINE.json configs[1], "C2"): the MovieLens-1M two-tower training
+step at emb_dim=128, batch 1024, 16 explicit negatives per user, hidden
+[256,128], dropout 0.2, tau 0.05, Adam(1e-3, wd 1e-5), clip 1.0
+(scripts/train_movielens.py:39-122 → TwoTowerTrainer.train_epoch,
+src/training/trainers/two_tower.py:98-146) on an ML-1M-shaped synthetic
+stream (ratings.dat is not available). One step = feature-row gather (fused)
++ user/pos/neg tower forward + fused 0.7·contrastive + 0.3·in-batch loss
+forward/backward + tower backward + clip + Adam, all on the MI355X kernels.
+pairs/step = B² (in-batch) + B·N (explicit) per GPU; N GPUs run data-parallel
+replicas on their own batches with one RCCL all-reduce of the flat grad slab
+(weak scaling).
+
+Extras on the same line (rank 0): Flat-IP top-K QPS at config 3 (6,040 users x
+3,416 items, fp32, k=10) and a config-4 shard (65,536 queries x 125,000
+items, fp16, k=100), the HBM row-gather rate (config-5 table shard, bf16
+rows of 256), the live roofline of the dominant kernel, and the CPU baseline
+(the oracle's torch-CPU restatement of the same step on this host's cores).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "real-time-recommendation-system-with-feature-store_amd")
+for p in (REPO, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_F32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector rate), MI355X_MICROARCH.md
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16/fp16 MFMA
+PEAK_HBM_GBS = 8000.0      # HBM3E spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world, torch.device("cuda", local)
+    return None, 0, 1, torch.device("cuda", 0)
+
+
+def c2_setup(dev, rank, n_batches):
+    from src.data.movielens import build_batches, feature_tables, synthetic_movielens
+    from src.training.utils import create_two_tower_model_for_training
+    data = synthetic_movielens(seed=0)
+    uf, mf = feature_tables(data)
+    bu, bp, bn = build_batches(data.train_interactions, data.num_movies, 1024, 16, n_batches, seed=100 + rank)
+    torch.manual_seed(1234)
+    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
+                                                        "dropout_rate": 0.2, "temperature": 0.05})
+    tables = (torch.from_numpy(uf).to(dev), torch.from_numpy(mf).to(dev))
+    batches = [tuple(torch.from_numpy(x[i]).to(dev) for x in (bu, bp, bn)) for i in range(n_batches)]
+    return model, tables, batches, (uf, mf, bu, bp, bn)
+
+
+def cpu_baseline(host, budget_s=10.0):
+    """The oracle's torch-CPU restatement of the reference step (same math as
+    src/training/trainers/two_tower.py:98-146) on a bounded sample of C2 batches."""
+    from oracle import two_tower as orc
+    from src.training.utils import create_two_tower_model_for_training
+    uf, mf, bu, bp, bn = host
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    torch.manual_seed(1234)
+    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
+                                                        "dropout_rate": 0.2, "temperature": 0.05})
+    us = {k: v.clone() for k, v in model.user_tower.state_dict().items()}
+    its = {k: v.clone() for k, v in model.item_tower.state_dict().items()}
+    biases = {"user_bias": torch.zeros(1), "item_bias": torch.zeros(1)}
+    opt = {}
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        i = steps % bu.shape[0]
+        u = torch.from_numpy(uf[bu[i]])
+        p = torch.from_numpy(mf[bp[i]])
+        n = torch.from_numpy(mf[bn[i]]).view(1024, 16, 20)
+        orc.train_step(us, its, biases, opt, u, p, n, temperature=0.05, dropout_p=0.2)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or steps >= 200:
+            break
+    pairs = steps * (1024 * 1024 + 1024 * 16)
+    return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} C2 train steps (B=1024, N=16, emb 128) of oracle/two_tower.train_step on "
+                      f"torch-CPU, {el:.1f}s", "ms_per_step": 1000.0 * el / steps}
+
+
+def topk_extras(dev):
+    from src import kernels
+    from src.profiling import TIMER
+    out = {}
+    g = torch.Generator(device=dev).manual_seed(7)
+    # config 3: 6040 x 3416 fp32, k=10
+    q = torch.nn.functional.normalize(torch.randn(6040, 128, device=dev, generator=g), dim=1)
+    x = torch.nn.functional.normalize(torch.randn(3416, 128, device=dev, generator=g), dim=1)
+    for _ in range(3):
+        kernels.flatip_topk(q, x, 10)
+    torch.cuda.synchronize()
+    TIMER.enable(["flatip_topk"])
+    reps = 20
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        kernels.flatip_topk(q, x, 10)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    s = TIMER.summary()["flatip_topk"]
+    TIMER.disable()
+    out["topk_c3"] = {"qps": 6040 / el, "ms": el * 1e3, "kernel_ms": s["avg_ms"],
+                      "tflops": s["flops"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e12, "dtype": "f32", "k": 10,
+                      "shape": "6040x3416x128"}
+    # config 4 shard: 65,536 queries x 125,000 items (1M / 8 GPUs), fp16, k=100
+    q = torch.nn.functional.normalize(torch.randn(65536, 128, device=dev, generator=g), dim=1).half()
+    x = torch.nn.functional.normalize(torch.randn(125000, 128, device=dev, generator=g), dim=1).half()
+    kernels.flatip_topk(q, x, 100)
+    torch.cuda.synchronize()
+    TIMER.enable(["flatip_topk"])
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        kernels.flatip_topk(q, x, 100)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    s = TIMER.summary()["flatip_topk"]
+    TIMER.disable()
+    tf = s["flops"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e12
+    out["topk_c4_shard"] = {"qps": 65536 / el, "ms": el * 1e3, "tflops": tf, "mfma_frac": tf / PEAK_BF16_TFLOPS,
+                            "dtype": "f16", "k": 100, "shape": "65536x125000x128"}
+    del q, x
+    # config 5 gather: bf16 rows of 256 from a 12.5M-row shard, 16M ids per launch
+    rows = 12_500_000
+    table = torch.empty((rows, 256), dtype=torch.bfloat16, device=dev)
+    table.view(torch.int16).random_(-30000, 30000, generator=g)
+    ids = torch.randint(0, rows, (16_777_216,), device=dev, generator=g)
+    outb = torch.empty((ids.numel(), 256), dtype=torch.bfloat16, device=dev)
+    kernels.gather_rows(table, ids, out=outb)
+    torch.cuda.synchronize()
+    TIMER.enable(["gather_rows"])
+    for _ in range(5):
+        kernels.gather_rows(table, ids, out=outb)
+    s = TIMER.summary()["gather_rows"]
+    TIMER.disable()
+    gbs = s["bytes"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e9
+    out["gather_c5"] = {"GBps": gbs, "hbm_frac": gbs / PEAK_HBM_GBS, "ms": s["avg_ms"], "ids": ids.numel(),
+                        "row_bytes": 512}
+    del table, ids, outb
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    dist, rank, world, dev = dist_setup(args.gpus)
+    torch.cuda.set_device(dev)
+    from src import native
+    from src.profiling import TIMER
+    from src.training.fused_step import FusedTrainStep
+    native.lib()
+
+    n_batches = min(args.steps + args.warmup, 64)
+    model, (ut, mt), batches, host = c2_setup(dev, rank, n_batches)
+    model.to(dev)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, max_norm=1.0,
+                          process_group=(dist.group.WORLD if dist is not None else None))
+
+    def run(i):
+        bu, bp, bn = batches[i % n_batches]
+        return step(ut, mt, mt, user_ids=bu, pos_ids=bp, neg_ids=bn)
+
+    for i in range(args.warmup):
+        run(i)
+    # calibration step (untimed): which ABI call dominates the step?
+    TIMER.enable()
+    run(args.warmup)
+    cal = TIMER.summary()
+    TIMER.disable()
+    dominant = max(cal, key=lambda k: cal[k]["total_ms"])
+
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    TIMER.enable([dominant])
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = run(i)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    live = TIMER.summary()
+    TIMER.disable()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss[0].item())
+
+    pairs_per_step = 1024 * 1024 + 1024 * 16
+    value = world * args.steps * pairs_per_step / elapsed
+    d = live[dominant]
+    per_launch_flops = d["flops"] / max(1, d["count"])
+    per_launch_bytes = d["bytes"] / max(1, d["count"])
+    avg_s = d["avg_ms"] * 1e-3
+    if per_launch_flops > 0:
+        achieved = per_launch_flops / avg_s / 1e12
+        roof = {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / PEAK_F32_TFLOPS, "traffic": None}
+    else:
+        achieved = per_launch_bytes / avg_s / 1e9
+        roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS, "traffic": None}
+    roof.update({"kernel": dominant, "launches_per_step": d["count"] / args.steps,
+                 "avg_launch_ms": d["avg_ms"], "step_share": cal[dominant]["total_ms"] /
+                 max(1e-9, sum(v["total_ms"] for v in cal.values())),
+                 "calibration_ms": {k: round(v["total_ms"], 4) for k, v in cal.items()}})
+
+    result = {
+        "metric": "user-item pairs scored/sec (train) + top-K queries/sec, emb_dim=128",
+        "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic ML-1M-shaped (6040 users x 3416 movies, seeded; ratings.dat unavailable)",
+        "config": {"workload": "C2: MovieLens-1M two-tower train step, emb 128, batch 1024, 16 negatives, "
+                               "hidden [256,128], dropout 0.2, tau 0.05, Adam+clip",
+                   "global_batch": 1024 * world, "emb_dim": 128, "num_negatives": 16,
+                   "parallelism": f"dp{world}", "final_loss": final_loss},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1:
+        if not args.no_extras:
+            try:
+                result["extras"] = topk_extras(dev)
+            except Exception as e:  # extras never hide the headline
+                result["extras"] = {"error": repr(e)}
+        if not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(host, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -76,7 +76,9 @@ int rt_l2_renorm_f32(float* x, int64_t n, int d, void* stream);
  * Brute-force inner-product top-K (faiss.IndexFlatIP.search,
  * src/serving/retrieval.py:96-98,171; and the masked np.dot + argsort of
  * scripts/evaluate_model.py:217-232).
- * queries [nq, d], items [nx, d], both `dtype`; d % 8 == 0, d <= 512; 1 <= k <= 1024.
+ * queries [nq, d], items [nx, d], both `dtype`, rows 16-byte aligned:
+ * f32: d % 4 == 0, d <= 128; f16/bf16: d % 8 == 0, d <= 256; 1 <= k <= 512;
+ * nx + id_offset < 2^32 - 1.
  * exclude_bits: optional uint32 bitmap [nq, exclude_words]; bit j of row q set
  *   means item j is skipped for query q.
  * Result rows: the first k of the (score desc, id asc) order (lower id wins
@@ -92,7 +94,7 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
 
 /* Merge n_lists candidate lists per query, layout [n_lists][nq][k_in] (as an
  * all_gather_into_tensor over ranks produces), into the (score desc, id asc)
- * top k_out. id -1 entries are ignored. k_in*n_lists <= 8192, k_out <= 1024. */
+ * top k_out. id -1 entries are ignored; ids must be < 2^32 - 1; k_out <= 512. */
 int rt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int n_lists, int k_in,
                   int k_out, float* out_scores, int64_t* out_ids, void* stream);
 
@@ -102,16 +104,18 @@ int rt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int n_lis
  * F.normalize(p=2, eps=1e-12).
  *
  * rt_linear_fwd_f32 computes one Linear with fused prologue/epilogue:
- *   A row r  = src[gather ? ids[r] : r]               (gather: fused row gather)
- *   if prev_mode != 0: a = drop(bn(act_prev(A)))      (previous hidden block)
- *      bn: train (prev_mode=1) batch stats from prev_stats (fp64 [2*k]: sum, sumsq
- *          of act_prev(z) over prev_m rows), biased var, eps; block 0 also writes
- *          save_mean/save_invstd [k] and updates running_mean/var (momentum);
- *          eval (prev_mode=2): running stats.
- *      drop: keep with prob 1-p, scale 1/(1-p), mask = hash(seed, row, col).
- *   z = a · Wᵀ + bias   (W [n, k] row-major)  → z_out [m, n]
- *   if stats_out: stats_out[c] += Σ_r act(z[r,c]), stats_out[n+c] += Σ act(z)^2 (fp64)
- *   if l2_out: l2_out[r] = z[r]/max(||z[r]||, 1e-12), norms_out[r] = ||z[r]||
+ *   A row r  = src[ids ? ids[r] : r]                  (ids: fused row gather)
+ *   prev_mode 0: a = A (raw input)
+ *             1: a = drop(bn(act_prev(A))), BN in train mode: batch mean/biased var
+ *                from prev_stats (fp64 [2k]: Σ act_prev(z), Σ act_prev(z)^2 over m
+ *                rows), eps; block 0 writes save_mean/save_invstd [k] and updates
+ *                running_mean/var (momentum, unbiased var) — BatchNorm1d.train()
+ *             2: same with running stats (eval); block 0 writes save_mean/invstd
+ *             3: a = drop(act_prev(A))   (no BN: ItemTower.content_projection)
+ *   drop: keep with prob 1-p, scale 1/(1-p), mask = hash(drop_seed, r, col)
+ *   z = a · Wᵀ + bias   (W [n, k] row-major, n <= 512)  → z_out [m, n]
+ *   stats_out (caller-zeroed fp64 [2n]) += (Σ_r act(z), Σ_r act(z)^2)
+ *   l2_out: F.normalize(z, p=2, eps=1e-12) rows, norms_out[r] = ||z[r]||
  * ------------------------------------------------------------------------ */
 typedef struct {
     const float* src;        /* [src_rows, ld_src] input rows (features or prev z) */
@@ -123,69 +127,71 @@ typedef struct {
     int n;                   /* output features                                        */
     const float* w;          /* [n, k]                                                 */
     const float* bias;       /* [n] or NULL                                            */
-    /* previous hidden block applied on load */
-    int prev_mode;           /* 0 none, 1 BN train, 2 BN eval                          */
+    int prev_mode;           /* 0 raw, 1 BN train, 2 BN eval, 3 act+dropout only        */
     int prev_act;            /* rt_act of the previous block                           */
     const double* prev_stats;/* [2k] fp64 sums (mode 1)                                */
     const float* bn_gamma;   /* [k]                                                    */
     const float* bn_beta;    /* [k]                                                    */
-    float* running_mean;     /* [k] updated in mode 1 (may be NULL)                    */
+    float* running_mean;     /* [k] read (mode 2) / updated (mode 1, may be NULL)      */
     float* running_var;      /* [k]                                                    */
-    float* save_mean;        /* [k] written in mode 1 (for backward)                   */
+    float* save_mean;        /* [k] written by block 0 (modes 1,2; may be NULL)        */
     float* save_invstd;      /* [k]                                                    */
     float bn_eps;
     float bn_momentum;
     float drop_p;            /* dropout prob of the previous block (0 = off)           */
-    uint64_t drop_seed;
-    /* outputs */
-    float* z_out;            /* [m, n] pre-activation (may be NULL if l2_out)         */
-    int act;                 /* activation of THIS block (for stats)                   */
-    double* stats_out;       /* [2n] accumulated, caller zeroes (NULL = skip)          */
+    uint64_t drop_seed;      /* mask seed = drop_seed + (*seed_offset if non-NULL)      */
+    const uint64_t* seed_offset; /* device counter (hipGraph replay draws new masks)   */
+    float* z_out;            /* [m, n] pre-activation, or NULL                         */
+    int act;                 /* activation of THIS block (for stats_out)               */
+    double* stats_out;       /* [2n] accumulated (NULL = skip)                         */
     float* l2_out;           /* [m, n] normalized rows (final layer) or NULL          */
-    float* norms_out;        /* [m] row norms (final layer) or NULL                    */
+    float* norms_out;        /* [m] row norms (with l2_out)                            */
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
 
-/* Backward of one Linear (+ the hidden block that feeds it):
- *   dz source: grad_mode 0 → dz = normalize_bwd(dout, l2_out, norms) (final layer);
- *              grad_mode 1 → dz = act'(z)·BNbwd(g) from g [m,n], z, bn save stats and
- *                            g_stats (fp64 [2n]: Σg, Σg·x̂) (hidden layer, train BN);
- *              grad_mode 2 → same with eval BN (dz = act'(z)·γ·invstd_running·g).
- *   dW += dzᵀ·a, dbias += Σ_r dz   (fp32 atomics into caller-zeroed buffers)
- *   if dgamma: dgamma += Σ g·x̂, dbeta += Σ g (this block's BN params, mode 1/2)
- *   if g_prev: g_prev = drop_bwd(dz·W) [m, k] and g_prev_stats += (Σg, Σg·x̂_prev)
- *              (x̂_prev from prev z with the prev block's saved stats)
- *   if dsrc (first layer only): dsrc = dz·W (input gradient, e.g. embeddings). */
+/* Backward of one Linear and of the block that produced its output gradient.
+ *   grad_mode 0: dz = normalize_bwd(dout; l2_out, norms)            (final layer)
+ *             1: dz = act'(z)·γ·invstd·(g − Σg/m − x̂·Σg·x̂/m)    (BN train; g_stats)
+ *             2: dz = act'(z)·γ·invstd·g                         (BN eval)
+ *             3: dz = act'(z)·g                                   (no BN)
+ *      with g = d loss/d(BN output) [m, n], x̂ = (act(z) − save_mean)·save_invstd.
+ *   dz_ws [m, n] receives dz; dbias += Σ_r dz; dw += dzᵀ·a  (fp32 atomics into
+ *   caller-zeroed buffers), a = the forward input of this Linear recomputed by
+ *   the same prologue (src/ids/prev_* exactly as passed to rt_linear_fwd_f32).
+ *   modes 1/2: dgamma += Σ g·x̂, dbeta += Σ g (read from g_stats).
+ *   da = dz·W [m, k] then: dsrc = da (if non-NULL; input gradient, layer 1) and/or
+ *   g_prev = drop_bwd_prev(da) with g_prev_stats += (Σ g_prev, Σ g_prev·x̂_prev)
+ *   (x̂_prev from src with prev_mean/prev_invstd; prev_mode 1/2 only).
+ *   n <= 256 and k <= 512. */
 typedef struct {
-    /* this layer */
     int64_t m; int k; int n;
     const float* w;          /* [n, k] */
     float* dw;               /* [n, k] accumulated */
     float* dbias;            /* [n] accumulated or NULL */
+    float* dz_ws;            /* [m, n] workspace */
     int grad_mode;
     const float* dout;       /* mode 0: [m, n] */
     const float* l2_out;     /* mode 0: [m, n] */
     const float* norms;      /* mode 0: [m] */
-    const float* g;          /* mode 1/2: [m, n] grad wrt this block's dropout output */
-    const float* z;          /* mode 1/2: [m, n] pre-activation of this block */
+    const float* g;          /* modes 1-3: [m, n] */
+    const float* z;          /* modes 1-3: [m, n] pre-activation of this block */
     int act;                 /* this block's activation */
-    const double* g_stats;   /* mode 1: [2n] */
-    const float* save_mean;  /* [n] this block's BN batch mean (mode 1) or running mean (2) */
-    const float* save_invstd;/* [n] this block's invstd (mode 1) or 1/sqrt(rv+eps) (2) */
+    const double* g_stats;   /* modes 1,2: [2n] (Σg, Σg·x̂) */
+    const float* save_mean;  /* [n] */
+    const float* save_invstd;/* [n] */
     const float* bn_gamma;   /* [n] */
     float* dgamma;           /* [n] accumulated or NULL */
     float* dbeta;            /* [n] */
-    float drop_p; uint64_t drop_seed; /* this block's dropout (applied to g already) */
-    /* the input A of this linear: recomputed exactly as the forward prologue */
+    /* the input A of this linear, recomputed exactly as the forward prologue */
     const float* src; int64_t src_rows; int ld_src; const int64_t* ids;
     int prev_mode; int prev_act;
-    const float* prev_mean; const float* prev_invstd;
+    const float* prev_mean; const float* prev_invstd;   /* prev block save_mean/invstd */
     const float* prev_gamma; const float* prev_beta;
-    float prev_drop_p; uint64_t prev_drop_seed;
+    float prev_drop_p; uint64_t prev_drop_seed; const uint64_t* seed_offset;
     /* outputs towards the previous block */
     float* g_prev;           /* [m, k] or NULL */
-    double* g_prev_stats;    /* [2k] accumulated, caller zeroes */
+    double* g_prev_stats;    /* [2k] accumulated, caller zeroes (NULL = skip) */
     float* dsrc;             /* [m, k] input grad (first layer), or NULL */
 } rt_linear_bwd_args;
 
@@ -199,8 +205,10 @@ int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);
  *     pos_i = u_i·p_i/τ + ub + ib ; neg_ij = u_i·q_ij/τ ; CE over [pos_i, neg_i·], label 0
  *   in-batch (in_batch_negative_loss, :453-479): S = U·Pᵀ/τ, CE(S, arange B)
  *   loss = w_explicit·L_explicit + w_in_batch·L_in_batch   (trainer :134)
- * and writes d loss / d{u, p, q, ub, ib} (grad buffers are OVERWRITTEN, except
- * dbias which is accumulated). n_neg = 0 disables the explicit term.
+ * and writes d loss / d{u, p, q} (OVERWRITTEN) and accumulates d loss / d{ub, ib}
+ * into d_user_bias / d_item_bias (may be NULL). n_neg = 0: the loss is the
+ * in-batch CE alone (weight 1, trainer fallback :136); w_in_batch = 0 skips
+ * the in-batch term (contrastive_loss alone).
  * loss_out: fp64 [3] = (loss, L_explicit, L_in_batch), caller zeroes.
  * Workspace: rt_twotower_loss_workspace_bytes(B).
  * ------------------------------------------------------------------------ */
@@ -208,8 +216,8 @@ size_t rt_twotower_loss_workspace_bytes(int64_t b, int d);
 int rt_twotower_loss_fwd_bwd(const void* u, const void* p, const void* q, int dtype, int64_t b,
                              int d, int n_neg, float inv_tau, const float* user_bias,
                              const float* item_bias, float w_explicit, float w_in_batch,
-                             double* loss_out, float* du, float* dp, float* dq, float* dbias,
-                             void* workspace, size_t workspace_bytes, void* stream);
+                             double* loss_out, float* du, float* dp, float* dq, float* d_user_bias,
+                             float* d_item_bias, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Forward-only variants (validation, TwoTowerModel.forward(compute_loss=True)). */
 int rt_twotower_loss_fwd(const void* u, const void* p, const void* q, int dtype, int64_t b, int d,
@@ -222,19 +230,22 @@ int rt_similarity_f32(const float* u, const float* v, int64_t b, int d, float in
                       const float* user_bias, const float* item_bias, float* out, void* stream);
 
 /* ------------------------------------------------------------------------
- * Optimiser (src/training/trainers/two_tower.py:60-64,144):
- * rt_grad_sqnorm: sumsq_out[t] = Σ g² over tensor t (fp64, caller zeroes) for the
- *   n_tensors slices [offsets[t], offsets[t+1]) of the flat grad buffer.
- * rt_clip_adam_step: coef = min(1, max_norm/(sqrt(Σ_t ||g_t||)+1e-6)) with
- *   ||g_t|| = sqrt(sumsq[t]) (torch clip_grad_norm_ order); then torch.optim.Adam
- *   (L2 weight decay, bias correction) on the flat fp32 param/grad/m/v buffers.
+ * Optimiser (src/training/trainers/two_tower.py:60-64,144) on ONE flat fp32
+ * parameter slab (all tower tensors + biases contiguous) and its grad slab:
+ * rt_grad_sqnorm: sumsq_out[t] += Σ g² over tensor t = [offsets[t], offsets[t+1])
+ *   (offsets: device int64 [n_tensors+1]; sumsq_out fp64, caller zeroes).
+ * rt_clip_adam_step: clip_grad_norm_(max_norm): coef = min(1, max_norm /
+ *   (sqrt(Σ_t sumsq[t]) + 1e-6)); then torch.optim.Adam with L2 weight decay and
+ *   bias correction on g·coef. The step count and learning rate are read from
+ *   device memory when step_dev / lr_dev are non-NULL (hipGraph replay), else
+ *   from `step` / `lr`.
  * ------------------------------------------------------------------------ */
 int rt_grad_sqnorm(const float* grads, const int64_t* offsets, int n_tensors, double* sumsq_out,
                    void* stream);
 int rt_clip_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                       int64_t n, const double* sumsq, int n_tensors, float max_norm, float lr,
-                      float beta1, float beta2, float eps, float weight_decay, int step,
-                      void* stream);
+                      const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,
+                      int step, const int32_t* step_dev, void* stream);
 
 #ifdef __cplusplus
 }

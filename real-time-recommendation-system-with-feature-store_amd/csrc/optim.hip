@@ -1,0 +1,99 @@
+// Fused optimiser step on the flat parameter slab:
+// torch.nn.utils.clip_grad_norm_(params, 1.0) + torch.optim.Adam(lr, weight_decay)
+// (src/training/trainers/two_tower.py:60-64, 144). Two launches per step
+// instead of one clip + ~36 per-tensor Adam updates.
+#include "rt_common.h"
+
+namespace rt {
+namespace optim {
+
+constexpr int kChunk = 4096;  // elements per block in the norm pass
+
+__global__ __launch_bounds__(256) void grad_sqnorm_kernel(const float* __restrict__ g,
+                                                          const int64_t* __restrict__ offsets,
+                                                          double* __restrict__ out) {
+    __shared__ double red[4];
+    const int t = blockIdx.y;
+    const int64_t lo = offsets[t], hi = offsets[t + 1];
+    if (lo + static_cast<int64_t>(blockIdx.x) * kChunk >= hi) return;  // uniform per block
+    double s = 0.0;
+    for (int64_t c0 = lo + static_cast<int64_t>(blockIdx.x) * kChunk; c0 < hi;
+         c0 += static_cast<int64_t>(gridDim.x) * kChunk) {
+        const int64_t c1 = (c0 + kChunk) < hi ? (c0 + kChunk) : hi;
+        for (int64_t e = c0 + threadIdx.x; e < c1; e += 256) {
+            const double v = g[e];
+            s += v * v;
+        }
+    }
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&out[t], red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        const double* __restrict__ sumsq, int n_tensors,
+                                                        float max_norm, float lr, const float* lr_dev, float b1,
+                                                        float b2, float eps, float wd, int step,
+                                                        const int32_t* step_dev) {
+    __shared__ float coef_s, step_size_s, bc2_sqrt_s;
+    if (threadIdx.x == 0) {
+        double tot = 0.0;
+        for (int t = 0; t < n_tensors; ++t) tot += sumsq[t];
+        const float total = static_cast<float>(sqrt(tot));
+        const float coef = max_norm / (total + 1e-6f);
+        coef_s = coef < 1.f ? coef : 1.f;
+        const int st = step_dev ? *step_dev : step;
+        const float lr_v = lr_dev ? *lr_dev : lr;
+        const double bc1 = 1.0 - pow(static_cast<double>(b1), st);
+        const double bc2 = 1.0 - pow(static_cast<double>(b2), st);
+        step_size_s = static_cast<float>(lr_v / bc1);
+        bc2_sqrt_s = static_cast<float>(sqrt(bc2));
+    }
+    __syncthreads();
+    const float coef = coef_s, step_size = step_size_s, bc2s = bc2_sqrt_s;
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < n; e += stride) {
+        const float pv = p[e];
+        float gv = g[e] * coef;
+        if (wd != 0.f) gv = gv + wd * pv;
+        const float mv = m[e] + (1.f - b1) * (gv - m[e]);          // exp_avg.lerp_(grad, 1-beta1)
+        const float vv = v[e] * b2 + (1.f - b2) * gv * gv;         // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+        const float denom = sqrtf(vv) / bc2s + eps;
+        m[e] = mv;
+        v[e] = vv;
+        p[e] = pv - step_size * (mv / denom);
+    }
+}
+
+}  // namespace optim
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" int rt_grad_sqnorm(const float* grads, const int64_t* offsets, int n_tensors, double* sumsq_out,
+                              void* stream) {
+    if (n_tensors < 0 || (n_tensors > 0 && (!grads || !offsets || !sumsq_out))) return RT_ERR_INVALID;
+    if (n_tensors == 0) return RT_OK;
+    // offsets live on the device: 64 blocks per tensor, each striding over chunks;
+    // blocks past a small tensor's end exit at once
+    const dim3 grid(64, static_cast<unsigned>(n_tensors));
+    hipLaunchKernelGGL(optim::grad_sqnorm_kernel, grid, dim3(256), 0, as_stream(stream), grads, offsets, sumsq_out);
+    return check_launch("grad_sqnorm_kernel");
+}
+
+extern "C" int rt_clip_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                                 const double* sumsq, int n_tensors, float max_norm, float lr, const float* lr_dev,
+                                 float beta1, float beta2, float eps, float weight_decay, int step,
+                                 const int32_t* step_dev, void* stream) {
+    if (n < 0 || !params || !grads || !exp_avg || !exp_avg_sq || !sumsq || n_tensors <= 0) return RT_ERR_INVALID;
+    if (!step_dev && step < 1) return RT_ERR_INVALID;
+    if (n == 0) return RT_OK;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(optim::clip_adam_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, as_stream(stream),
+                       params, grads, exp_avg, exp_avg_sq, n, sumsq, n_tensors, max_norm, lr, lr_dev, beta1, beta2,
+                       eps, weight_decay, step, step_dev);
+    return check_launch("clip_adam_kernel");
+}

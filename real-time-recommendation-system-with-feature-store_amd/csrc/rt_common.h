@@ -55,6 +55,10 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// order LDS traffic of one wave: DS ops of a wave complete in order; this also
+// stops the compiler from hoisting reads above earlier writes by other lanes
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // ---- counter-based RNG for dropout masks (splitmix64 finaliser) ----
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;

@@ -16,10 +16,6 @@ struct Cand {
 
 __device__ __forceinline__ bool better(const Cand& a, const Cand& b) { return better(a.s, a.i, b.s, b.i); }
 
-// order LDS traffic of one wave (DS ops of a wave complete in order; this stops
-// the compiler from moving reads above the previous stage's writes)
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
 // Sort buf[0, n) (n a power of two >= 2) in LDS, better first. Whole wave calls.
 __device__ inline void wave_sort_lds(Cand* buf, int n) {
     const int lane = threadIdx.x & 63;

@@ -14,6 +14,7 @@ import torch
 
 from . import native
 from .native import call, ptr, stream_of
+from .profiling import TIMER
 
 # ---------------------------------------------------------------------------
 # workspace cache (grow-only, per device): no allocation inside hot calls
@@ -52,8 +53,9 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor, row_begin: int = 0,
         out = torch.empty((ids.numel(),) + tuple(row_shape), dtype=table.dtype, device=table.device)
     if check and oob is None:
         oob = torch.zeros(1, dtype=torch.int32, device=table.device)
-    call("rt_gather_rows", ptr(table), row_begin, table.shape[0], row_bytes, ptr(ids), ids.numel(),
-         ptr(out), ptr(oob), stream_of(table))
+    with TIMER.region("gather_rows", bytes_=2.0 * ids.numel() * row_bytes + 8.0 * ids.numel()):
+        call("rt_gather_rows", ptr(table), row_begin, table.shape[0], row_bytes, ptr(ids), ids.numel(),
+             ptr(out), ptr(oob), stream_of(table))
     if check and int(oob.item()) != 0:
         raise IndexError(f"{int(oob.item())} ids out of range for table of {table.shape[0]} rows")
     return out.view(tuple(ids.shape) + tuple(row_shape))
@@ -116,8 +118,10 @@ def flatip_topk(queries: torch.Tensor, items: torch.Tensor, k: int,
         words = exclude_bits.shape[1]
     nbytes = native.lib().rt_flatip_topk_workspace_bytes(nq, nx, d, dt, k)
     ws = workspace(queries.device, nbytes, "topk")
-    call("rt_flatip_topk", ptr(queries), nq, ptr(items) if nx else None, nx, d, dt, k, ptr(exclude_bits),
-         words, id_offset, ptr(scores), ptr(ids), ptr(ws), ws.numel(), stream_of(queries))
+    with TIMER.region("flatip_topk", flops=2.0 * nq * nx * d,
+                      bytes_=float((nq + nx) * d * queries.element_size() + nq * k * 12)):
+        call("rt_flatip_topk", ptr(queries), nq, ptr(items) if nx else None, nx, d, dt, k, ptr(exclude_bits),
+             words, id_offset, ptr(scores), ptr(ids), ptr(ws), ws.numel(), stream_of(queries))
     return scores, ids
 
 

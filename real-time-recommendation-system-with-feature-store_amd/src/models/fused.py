@@ -1,0 +1,376 @@
+"""Host-side executor of the fused tower MLP kernels (rt_linear_fwd_f32 /
+rt_linear_bwd_f32) and the flat parameter slab.
+
+A tower's ``mlp`` (src/models/two_tower.py:56-72: [Linear → act → BatchNorm1d →
+Dropout] × L → Linear) is run as L+1 kernel launches forward and 2(L+1)
+backward; the row gather of the input features (layer 1), BatchNorm (batch
+statistics finalised from fp64 column sums), activation, dropout and the final
+F.normalize are fused into those launches. Parameter gradients are
+accumulated straight into one flat fp32 grad slab (views are the params'
+``.grad``), so the optimiser is one fused clip+Adam kernel.
+"""
+from __future__ import annotations
+
+import ctypes
+import itertools
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from .. import native
+from ..native import LinearBwdArgs, LinearFwdArgs, call, ptr
+from ..profiling import TIMER
+
+ACT_CODE = {nn.ReLU: 0, nn.GELU: 1, nn.LeakyReLU: 2, nn.Tanh: 3, nn.Sigmoid: 4}
+ACT_NONE = 5
+
+_seed_counter = itertools.count(1)
+
+
+def act_code(mod: Optional[nn.Module]) -> int:
+    if mod is None:
+        return ACT_NONE
+    for cls, code in ACT_CODE.items():
+        if isinstance(mod, cls):
+            if cls is nn.LeakyReLU and abs(mod.negative_slope - 0.1) > 1e-12:
+                raise NotImplementedError("LeakyReLU slope other than 0.1 (two_tower.py:82)")
+            return code
+    raise NotImplementedError(f"activation {type(mod).__name__}")
+
+
+@dataclass
+class Block:
+    """One Linear plus the (optional) act/BN/dropout that FOLLOW it."""
+    linear: nn.Linear
+    act: int = ACT_NONE
+    bn: Optional[nn.BatchNorm1d] = None
+    drop: Optional[nn.Dropout] = None
+
+    def drop_p(self) -> float:
+        return float(self.drop.p) if (self.drop is not None and self.drop.training and self.drop.p > 0) else 0.0
+
+    def bn_mode(self) -> int:
+        """prologue/grad mode of this block's BN for the consumer: 1 train, 2 eval, 3 none."""
+        if self.bn is None:
+            return 3
+        return 1 if self.bn.training else 2
+
+
+def blocks_from_sequential(seq: nn.Sequential) -> List[Block]:
+    """[Linear, act, BN, Dropout]*L + Linear (two_tower.py:60-70) or the content
+    projection Linear, ReLU, Dropout, Linear (:185-190)."""
+    mods = list(seq)
+    blocks: List[Block] = []
+    i = 0
+    while i < len(mods):
+        lin = mods[i]
+        if not isinstance(lin, nn.Linear):
+            raise NotImplementedError(f"unexpected module {type(lin).__name__} at {i}")
+        b = Block(lin)
+        i += 1
+        if i < len(mods) and not isinstance(mods[i], (nn.Linear, nn.BatchNorm1d, nn.Dropout)):
+            b.act = act_code(mods[i])
+            i += 1
+        if i < len(mods) and isinstance(mods[i], nn.BatchNorm1d):
+            b.bn = mods[i]
+            i += 1
+        if i < len(mods) and isinstance(mods[i], nn.Dropout):
+            b.drop = mods[i]
+            i += 1
+        blocks.append(b)
+    return blocks
+
+
+# ---------------------------------------------------------------------------
+# parameter slab
+# ---------------------------------------------------------------------------
+class ParamSlab:
+    """All parameters of a module in ONE contiguous fp32 device buffer (plus a
+    grad slab). Params become views (``p.data``), and ``p.grad`` is pinned to the
+    grad-slab view whenever the kernels need it."""
+
+    def __init__(self, module: nn.Module):
+        self.module = module
+        self.params: List[nn.Parameter] = []
+        self.data: Optional[torch.Tensor] = None
+        self.grad: Optional[torch.Tensor] = None
+        self.offsets: List[int] = []
+        self.offsets_dev: Optional[torch.Tensor] = None
+
+    def _valid(self) -> bool:
+        ps = [p for p in self.module.parameters()]
+        if self.data is None or len(ps) != len(self.params) or any(a is not b for a, b in zip(ps, self.params)):
+            return False
+        base = self.data.data_ptr()
+        for p, off in zip(self.params, self.offsets):
+            if p.device != self.data.device or p.data_ptr() != base + off * 4:
+                return False
+        return True
+
+    def ensure(self) -> "ParamSlab":
+        if self._valid():
+            return self
+        ps = list(self.module.parameters())
+        if not ps:
+            raise ValueError("module has no parameters")
+        dev = ps[0].device
+        for p in ps:
+            if p.dtype != torch.float32 or p.device != dev:
+                raise TypeError("parameter slab needs fp32 parameters on one device")
+        sizes = [p.numel() for p in ps]
+        # 16-byte aligned starts (vector loads in the kernels)
+        offs, cur = [], 0
+        for s in sizes:
+            offs.append(cur)
+            cur += (s + 3) // 4 * 4
+        data = torch.zeros(cur, dtype=torch.float32, device=dev)
+        grad = torch.zeros(cur, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, o, s in zip(ps, offs, sizes):
+                data[o:o + s].copy_(p.data.reshape(-1))
+        for p, o, s in zip(ps, offs, sizes):
+            p.data = data[o:o + s].view(p.shape)
+            old = p.grad
+            p.grad = grad[o:o + s].view(p.shape)
+            if old is not None:
+                p.grad.copy_(old)
+        self.params, self.offsets, self.data, self.grad = ps, offs, data, grad
+        ends = [o + s for o, s in zip(offs, sizes)]
+        self.bounds = list(zip(offs, ends))
+        self.offsets_dev = None
+        return self
+
+    def attach_grads(self):
+        """Make every param's .grad the slab view again (after zero_grad(set_to_none))."""
+        self.ensure()
+        for p, (o, e) in zip(self.params, self.bounds):
+            view = self.grad[o:e]
+            if p.grad is None:
+                view.zero_()
+                p.grad = view.view(p.shape)
+            elif p.grad.data_ptr() != view.data_ptr():
+                view.copy_(p.grad.reshape(-1))
+                p.grad = view.view(p.shape)
+
+    def grad_of(self, p: torch.Tensor) -> torch.Tensor:
+        for q, (o, e) in zip(self.params, self.bounds):
+            if q is p:
+                return self.grad[o:e].view(p.shape)
+        raise KeyError("parameter not in slab")
+
+    def tensor_offsets(self) -> torch.Tensor:
+        """Device int64 [n+1] boundaries (per-tensor grad norms; the alignment
+        padding between tensors is zero in both slabs)."""
+        if self.offsets_dev is None:
+            b = [o for o, _ in self.bounds] + [self.bounds[-1][1]]
+            self.offsets_dev = torch.tensor(b, dtype=torch.int64, device=self.data.device)
+        return self.offsets_dev
+
+
+# ---------------------------------------------------------------------------
+# chain executor
+# ---------------------------------------------------------------------------
+@dataclass
+class ChainCtx:
+    m: int
+    src: torch.Tensor
+    ids: Optional[torch.Tensor]
+    zs: List[Optional[torch.Tensor]] = field(default_factory=list)
+    save_mean: List[Optional[torch.Tensor]] = field(default_factory=list)
+    save_invstd: List[Optional[torch.Tensor]] = field(default_factory=list)
+    seeds: List[int] = field(default_factory=list)
+    drop_ps: List[float] = field(default_factory=list)
+    bn_modes: List[int] = field(default_factory=list)
+    out: Optional[torch.Tensor] = None
+    norms: Optional[torch.Tensor] = None
+    normalize: bool = True
+
+
+def _stream(t: torch.Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
+                  normalize: bool = True, seed_offset: Optional[torch.Tensor] = None) -> ChainCtx:
+    """Run the block chain. ``src`` is the dense input [rows, k0] (fp32) or a
+    feature table when ``ids`` selects its rows (fused gather)."""
+    native.require_device(src, what="tower forward")
+    if src.dtype != torch.float32:
+        raise TypeError("tower input must be fp32 (the reference towers are fp32)")
+    src = src.contiguous()
+    m = int(ids.numel()) if ids is not None else int(src.shape[0])
+    if ids is not None:
+        ids = ids.contiguous().to(torch.int64)
+    dev = src.device
+    L = len(blocks) - 1
+    k0 = blocks[0].linear.in_features
+    if src.dim() != 2 or src.shape[1] != k0:
+        # what F.linear raises for the same mismatch
+        raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({m}x{src.shape[-1]} and "
+                           f"{k0}x{blocks[0].linear.out_features})")
+    for b in blocks[:-1]:
+        if b.bn is not None and b.bn.training and m <= 1:
+            raise ValueError("Expected more than 1 value per channel when training (BatchNorm1d)")
+    ctx = ChainCtx(m=m, src=src, ids=ids, normalize=normalize)
+    # one fp64 arena for all BN column sums of this call
+    widths = [b.linear.out_features for b in blocks[:-1]]
+    stats_arena = torch.zeros(max(1, 2 * sum(widths)), dtype=torch.float64, device=dev)
+    stats, off = [], 0
+    for wdt in widths:
+        stats.append(stats_arena[off:off + 2 * wdt])
+        off += 2 * wdt
+    st = _stream(src)
+    cur_src, cur_ids, ld = src, ids, src.shape[1]
+    for li, b in enumerate(blocks):
+        lin = b.linear
+        a = LinearFwdArgs()
+        a.src = cur_src.data_ptr()
+        a.src_rows = cur_src.shape[0]
+        a.ld_src = ld
+        a.ids = cur_ids.data_ptr() if cur_ids is not None else None
+        a.m = m
+        a.k = lin.in_features
+        a.n = lin.out_features
+        a.w = lin.weight.data_ptr()
+        a.bias = lin.bias.data_ptr() if lin.bias is not None else None
+        a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
+        if li == 0:
+            a.prev_mode = 0
+        else:
+            pb = blocks[li - 1]
+            a.prev_mode = pb.bn_mode()
+            a.prev_act = pb.act
+            a.drop_p = pb.drop_p()
+            a.drop_seed = ctx.seeds[li - 1]
+            if pb.bn is not None:
+                a.prev_stats = stats[li - 1].data_ptr()
+                a.bn_gamma = pb.bn.weight.data_ptr()
+                a.bn_beta = pb.bn.bias.data_ptr()
+                a.running_mean = pb.bn.running_mean.data_ptr()
+                a.running_var = pb.bn.running_var.data_ptr()
+                sm = torch.empty(lin.in_features, dtype=torch.float32, device=dev)
+                si = torch.empty(lin.in_features, dtype=torch.float32, device=dev)
+                ctx.save_mean[li - 1], ctx.save_invstd[li - 1] = sm, si
+                a.save_mean = sm.data_ptr()
+                a.save_invstd = si.data_ptr()
+                a.bn_eps = float(pb.bn.eps)
+                a.bn_momentum = float(pb.bn.momentum if pb.bn.momentum is not None else 0.1)
+                if pb.bn.training:
+                    pb.bn.num_batches_tracked.add_(1)
+        a.act = b.act
+        if li < L:
+            z = torch.empty((m, lin.out_features), dtype=torch.float32, device=dev)
+            a.z_out = z.data_ptr()
+            if b.bn is not None and b.bn.training:
+                a.stats_out = stats[li].data_ptr()
+            ctx.zs.append(z)
+            ctx.save_mean.append(None)
+            ctx.save_invstd.append(None)
+            ctx.seeds.append(next(_seed_counter) * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
+            ctx.drop_ps.append(b.drop_p())
+            ctx.bn_modes.append(b.bn_mode())
+            cur_src, cur_ids, ld = z, None, lin.out_features
+        else:
+            out = torch.empty((m, lin.out_features), dtype=torch.float32, device=dev)
+            if normalize:
+                norms = torch.empty(m, dtype=torch.float32, device=dev)
+                a.l2_out = out.data_ptr()
+                a.norms_out = norms.data_ptr()
+                ctx.norms = norms
+            else:
+                a.z_out = out.data_ptr()
+            ctx.out = out
+        with TIMER.region("linear_fwd", flops=2.0 * m * a.k * a.n, bytes_=4.0 * (m * a.k + a.n * a.k + m * a.n)):
+            call("rt_linear_fwd_f32", ctypes.byref(a), st)
+    return ctx
+
+
+def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab: ParamSlab,
+                   want_dsrc: bool = False, seed_offset: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+    """Backward through the chain; parameter grads are atomically accumulated
+    into the slab. Returns d src (dense input) when ``want_dsrc``."""
+    dev = dout.device
+    dout = dout.contiguous()
+    m = ctx.m
+    L = len(blocks) - 1
+    st = _stream(dout)
+    slab.attach_grads()
+    max_w = max(b.linear.out_features for b in blocks)
+    dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev)
+    widths = [b.linear.out_features for b in blocks[:-1]]
+    gst_arena = torch.zeros(max(1, 2 * sum(widths)), dtype=torch.float64, device=dev)
+    gstats, off = [], 0
+    for wdt in widths:
+        gstats.append(gst_arena[off:off + 2 * wdt])
+        off += 2 * wdt
+    gs: List[Optional[torch.Tensor]] = [None] * L
+    dsrc = torch.empty((m, blocks[0].linear.in_features), dtype=torch.float32, device=dev) if want_dsrc else None
+    for li in range(L, -1, -1):
+        b = blocks[li]
+        lin = b.linear
+        a = LinearBwdArgs()
+        a.m, a.k, a.n = m, lin.in_features, lin.out_features
+        a.w = lin.weight.data_ptr()
+        a.dw = slab.grad_of(lin.weight).data_ptr()
+        a.dbias = slab.grad_of(lin.bias).data_ptr() if lin.bias is not None else None
+        a.dz_ws = dz_ws.data_ptr()
+        a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
+        if li == L:
+            if ctx.normalize:
+                a.grad_mode = 0
+                a.dout = dout.data_ptr()
+                a.l2_out = ctx.out.data_ptr()
+                a.norms = ctx.norms.data_ptr()
+            else:
+                a.grad_mode = 3
+                a.g = dout.data_ptr()
+                a.z = dout.data_ptr()
+                a.act = ACT_NONE
+        else:
+            a.grad_mode = ctx.bn_modes[li]
+            a.g = gs[li].data_ptr()
+            a.z = ctx.zs[li].data_ptr()
+            a.act = b.act
+            if b.bn is not None:
+                a.g_stats = gstats[li].data_ptr()
+                a.save_mean = ctx.save_mean[li].data_ptr()
+                a.save_invstd = ctx.save_invstd[li].data_ptr()
+                a.bn_gamma = b.bn.weight.data_ptr()
+                a.dgamma = slab.grad_of(b.bn.weight).data_ptr()
+                a.dbeta = slab.grad_of(b.bn.bias).data_ptr()
+        # input of this linear (recomputed by the same prologue as forward)
+        if li == 0:
+            a.src = ctx.src.data_ptr()
+            a.src_rows = ctx.src.shape[0]
+            a.ld_src = ctx.src.shape[1]
+            a.ids = ctx.ids.data_ptr() if ctx.ids is not None else None
+            a.prev_mode = 0
+            if want_dsrc:
+                if ctx.ids is not None:
+                    raise NotImplementedError("input gradient through a fused gather")
+                a.dsrc = dsrc.data_ptr()
+        else:
+            pb = blocks[li - 1]
+            a.src = ctx.zs[li - 1].data_ptr()
+            a.src_rows = m
+            a.ld_src = pb.linear.out_features
+            a.prev_mode = ctx.bn_modes[li - 1]
+            a.prev_act = pb.act
+            a.prev_drop_p = ctx.drop_ps[li - 1]
+            a.prev_drop_seed = ctx.seeds[li - 1]
+            if pb.bn is not None:
+                a.prev_mean = ctx.save_mean[li - 1].data_ptr()
+                a.prev_invstd = ctx.save_invstd[li - 1].data_ptr()
+                a.prev_gamma = pb.bn.weight.data_ptr()
+                a.prev_beta = pb.bn.bias.data_ptr()
+                a.g_prev_stats = gstats[li - 1].data_ptr()
+            g = torch.empty((m, pb.linear.out_features), dtype=torch.float32, device=dev)
+            gs[li - 1] = g
+            a.g_prev = g.data_ptr()
+        da = a.g_prev is not None or a.dsrc is not None
+        with TIMER.region("linear_bwd", flops=(4.0 if da else 2.0) * m * a.k * a.n,
+                          bytes_=4.0 * (3 * m * a.n + m * a.k * (2 if da else 1) + 2 * a.n * a.k)):
+            call("rt_linear_bwd_f32", ctypes.byref(a), st)
+    return dsrc

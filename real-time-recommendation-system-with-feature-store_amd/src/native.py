@@ -48,20 +48,20 @@ class LinearFwdArgs(ctypes.Structure):
         ("prev_mode", c_int), ("prev_act", c_int), ("prev_stats", vp), ("bn_gamma", vp), ("bn_beta", vp),
         ("running_mean", vp), ("running_var", vp), ("save_mean", vp), ("save_invstd", vp),
         ("bn_eps", c_f32), ("bn_momentum", c_f32), ("drop_p", c_f32), ("drop_seed", c_u64),
-        ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
+        ("seed_offset", vp), ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
     ]
 
 
 class LinearBwdArgs(ctypes.Structure):
     _fields_ = [
-        ("m", c_i64), ("k", c_int), ("n", c_int), ("w", vp), ("dw", vp), ("dbias", vp),
+        ("m", c_i64), ("k", c_int), ("n", c_int), ("w", vp), ("dw", vp), ("dbias", vp), ("dz_ws", vp),
         ("grad_mode", c_int), ("dout", vp), ("l2_out", vp), ("norms", vp),
         ("g", vp), ("z", vp), ("act", c_int), ("g_stats", vp), ("save_mean", vp), ("save_invstd", vp),
-        ("bn_gamma", vp), ("dgamma", vp), ("dbeta", vp), ("drop_p", c_f32), ("drop_seed", c_u64),
+        ("bn_gamma", vp), ("dgamma", vp), ("dbeta", vp),
         ("src", vp), ("src_rows", c_i64), ("ld_src", c_int), ("ids", vp),
         ("prev_mode", c_int), ("prev_act", c_int), ("prev_mean", vp), ("prev_invstd", vp),
         ("prev_gamma", vp), ("prev_beta", vp), ("prev_drop_p", c_f32), ("prev_drop_seed", c_u64),
-        ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp),
+        ("seed_offset", vp), ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp),
     ]
 
 
@@ -81,13 +81,13 @@ SIGNATURES = {
     "rt_linear_bwd_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_twotower_loss_workspace_bytes": (c_size, [c_i64, c_int]),
     "rt_twotower_loss_fwd_bwd": (c_int, [vp, vp, vp, c_int, c_i64, c_int, c_int, c_f32, vp, vp, c_f32,
-                                         c_f32, vp, vp, vp, vp, vp, vp, c_size, vp]),
+                                         c_f32, vp, vp, vp, vp, vp, vp, vp, c_size, vp]),
     "rt_twotower_loss_fwd": (c_int, [vp, vp, vp, c_int, c_i64, c_int, c_int, c_f32, vp, vp, c_f32, c_f32,
                                      vp, vp, c_size, vp]),
     "rt_similarity_f32": (c_int, [vp, vp, c_i64, c_int, c_f32, vp, vp, vp, vp]),
     "rt_grad_sqnorm": (c_int, [vp, vp, c_int, vp, vp]),
-    "rt_clip_adam_step": (c_int, [vp, vp, vp, vp, c_i64, vp, c_int, c_f32, c_f32, c_f32, c_f32, c_f32,
-                                  c_f32, c_int, vp]),
+    "rt_clip_adam_step": (c_int, [vp, vp, vp, vp, c_i64, vp, c_int, c_f32, c_f32, vp, c_f32, c_f32, c_f32,
+                                  c_f32, c_int, vp, vp]),
 }
 
 _lib = None

@@ -1,0 +1,163 @@
+"""One mixed-loss training step of ``TwoTowerTrainer.train_epoch``
+(src/training/trainers/two_tower.py:98-146) as a fixed sequence of gfx950
+launches, with no autograd and no torch compute:
+
+  user tower fwd │ pos item tower fwd │ neg item tower fwd   (gather fused into layer 1)
+  fused loss fwd+bwd (0.7·contrastive + 0.3·in-batch)          rt_twotower_loss_fwd_bwd
+  neg / pos / user tower bwd  (grads → flat slab, atomics)      rt_linear_bwd_f32 × 2(L+1) each
+  clip_grad_norm_(1.0) + Adam(lr, wd)                           rt_grad_sqnorm + rt_clip_adam_step
+
+Parameters, grads and Adam moments live in flat fp32 slabs; the step counter
+and learning rate live on the device so the whole step can be captured in a
+hipGraph and replayed (``capture``/``replay``).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional
+
+import torch
+
+from .. import kernels, native
+from ..models.fused import blocks_from_sequential, chain_backward, chain_forward
+from ..models.two_tower import TwoTowerModel
+from ..native import call, ptr
+from ..profiling import TIMER
+
+
+class FusedTrainStep:
+    def __init__(self, model: TwoTowerModel, lr: float = 1e-3, weight_decay: float = 1e-5, max_norm: float = 1.0,
+                 betas=(0.9, 0.999), eps: float = 1e-8, explicit_weight: float = 0.7,
+                 in_batch_weight: float = 0.3, process_group=None):
+        self.model = model
+        self.pg = process_group
+        self.slab = model.slab()
+        dev = self.slab.data.device
+        native.require_device(self.slab.data, what="FusedTrainStep")
+        self.dev = dev
+        self.exp_avg = torch.zeros_like(self.slab.data)
+        self.exp_avg_sq = torch.zeros_like(self.slab.data)
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.lr_dev = torch.tensor([lr], dtype=torch.float32, device=dev)
+        self.seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # dropout mask counter
+        self.sumsq = torch.zeros(len(self.slab.params), dtype=torch.float64, device=dev)
+        self.loss_buf = torch.zeros(3, dtype=torch.float64, device=dev)
+        self.lr, self.wd, self.max_norm = lr, weight_decay, max_norm
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.we, self.wb = explicit_weight, in_batch_weight
+        self.steps = 0
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.static: Dict[str, torch.Tensor] = {}
+
+    def set_lr(self, lr: float):
+        self.lr = lr
+        self.lr_dev.fill_(lr)
+
+    # ------------------------------------------------------------------
+    def _run(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None):
+        m = self.model
+        ub = blocks_from_sequential(m.user_tower.mlp)
+        ib = blocks_from_sequential(m.item_tower.mlp)
+        slab = self.slab
+        st = native.stream_of(slab.data)
+        self.step_dev.add_(1)
+        self.seed_dev.add_(1)
+        slab.grad.zero_()
+        so = self.seed_dev
+        u = chain_forward(ub, user_src, user_ids, seed_offset=so)
+        p = chain_forward(ib, pos_src, pos_ids, seed_offset=so)
+        q = chain_forward(ib, neg_src, neg_ids, seed_offset=so) if (neg_src is not None) else None
+        b, d = u.out.shape
+        n_neg = (q.m // b) if q is not None else 0
+        du = torch.empty_like(u.out)
+        dp = torch.empty_like(p.out)
+        dq = torch.empty_like(q.out) if q is not None else None
+        self.loss_buf.zero_()
+        ws = kernels.workspace(self.dev, native.lib().rt_twotower_loss_workspace_bytes(b, d), "loss")
+        ubias, ibias = m.user_bias, m.item_bias
+        with TIMER.region("loss_fwd_bwd", flops=6.0 * b * b * d + 6.0 * b * (n_neg + 1) * d,
+                          bytes_=4.0 * d * (4 * b + 2 * b * n_neg)):
+            call("rt_twotower_loss_fwd_bwd", ptr(u.out), ptr(p.out), ptr(q.out) if q is not None else None, 0, b,
+                 d, n_neg, 1.0 / m.temperature, ptr(ubias), ptr(ibias), self.we, self.wb, ptr(self.loss_buf),
+                 ptr(du), ptr(dp), ptr(dq),
+                 ptr(slab.grad_of(ubias)) if ubias is not None else None,
+                 ptr(slab.grad_of(ibias)) if ibias is not None else None, ptr(ws), ws.numel(), st)
+        if q is not None:
+            chain_backward(ib, q, dq, slab, seed_offset=so)
+        chain_backward(ib, p, dp, slab, seed_offset=so)
+        chain_backward(ub, u, du, slab, seed_offset=so)
+        if self.pg is not None:  # data parallel: average the flat grad slab (one RCCL all-reduce)
+            import torch.distributed as dist
+            dist.all_reduce(slab.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            slab.grad.mul_(1.0 / dist.get_world_size(self.pg))
+        self.sumsq.zero_()
+        nb = slab.data.numel() * 4.0
+        with TIMER.region("clip_adam", flops=0.0, bytes_=nb * 7):
+            call("rt_grad_sqnorm", ptr(slab.grad), ptr(slab.tensor_offsets()), len(slab.params), ptr(self.sumsq),
+                 st)
+            call("rt_clip_adam_step", ptr(slab.data), ptr(slab.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
+                 slab.data.numel(), ptr(self.sumsq), len(slab.params), self.max_norm, self.lr, ptr(self.lr_dev),
+                 self.b1, self.b2, self.eps, self.wd, 1, ptr(self.step_dev), st)
+        return self.loss_buf
+
+    def __call__(self, user_src: torch.Tensor, pos_src: torch.Tensor, neg_src: Optional[torch.Tensor],
+                 user_ids: Optional[torch.Tensor] = None, pos_ids: Optional[torch.Tensor] = None,
+                 neg_ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Dense features ([B,Fu], [B,Fi], [B*N,Fi] or [B,N,Fi]) or feature tables
+        with row ids (fused gather). Returns the device fp64 [3] loss buffer
+        (loss, explicit, in-batch) — read it only when needed (sync)."""
+        self.model.train()
+        if neg_src is not None and neg_ids is None and neg_src.dim() == 3:
+            neg_src = neg_src.reshape(-1, neg_src.shape[-1])
+        self.steps += 1
+        return self._run(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
+
+    # ------------------------------------------------------------------
+    # hipGraph capture of the whole step (ids/features in static buffers)
+    def capture(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None, warmup: int = 2):
+        self.model.train()
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._run(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._run(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
+        self.graph = g
+        self.steps += warmup + 1
+        return g
+
+    def replay(self):
+        self.graph.replay()
+        self.steps += 1
+        return self.loss_buf
+
+
+def smoke_check(dev: torch.device):
+    """Tiny train step vs the CPU oracle (called by __graft_entry__.smoke)."""
+    import numpy as np
+    from oracle import two_tower as orc
+    from ..training.utils import create_two_tower_model_for_training
+    torch.manual_seed(0)
+    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 32, "hidden_layers": [64, 32],
+                                                        "dropout_rate": 0.0, "temperature": 0.05})
+    us = {k: v.clone() for k, v in model.user_tower.state_dict().items()}
+    its = {k: v.clone() for k, v in model.item_tower.state_dict().items()}
+    g = torch.Generator().manual_seed(1)
+    uf = torch.randn(32, 3, generator=g)
+    pf = torch.rand(32, 20, generator=g)
+    nf = torch.rand(32, 4, 20, generator=g)
+    ref = orc.train_step(us, its, {"user_bias": torch.zeros(1), "item_bias": torch.zeros(1)}, {}, uf, pf, nf,
+                         temperature=0.05)
+    model.to(dev)
+    step = FusedTrainStep(model)
+    loss = step(uf.to(dev), pf.to(dev), nf.to(dev))
+    torch.cuda.synchronize()
+    got = float(loss[0].item())
+    assert abs(got - ref["loss"]) <= 1e-4 * abs(ref["loss"]), (got, ref["loss"])
+    w_ref = us["mlp.0.weight"].numpy()
+    w_got = model.user_tower.mlp[0].weight.detach().cpu().numpy()
+    np.testing.assert_allclose(w_got, w_ref, rtol=1e-3, atol=1e-5)
