@@ -77,7 +77,9 @@ def test_tower_golden_eval_train_backward(dev, golden, name):
         ref = g.get(f"grad/{k}")
         if ref is None:
             continue
-        np.testing.assert_allclose(p.grad.cpu().numpy(), ref, rtol=1e-3, atol=2e-5, err_msg=k)
+        # fp32 reductions in a different order: tolerance relative to the gradient's scale
+        np.testing.assert_allclose(p.grad.cpu().numpy(), ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max() + 1e-7,
+                                   err_msg=k)
     sd = t.state_dict()
     for k, v in g.items():
         if k.startswith("post/"):

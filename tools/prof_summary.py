@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 kernel trace (``--kernel-trace`` .db or
+``kernel_stats.csv``/``kernel_trace.csv``) into a per-kernel table
+(calls, total/avg/min/max µs, share) for profiles/.
+
+Usage: python tools/prof_summary.py <results.db | kernel_trace.csv> [--out profiles/x.md]
+"""
+import argparse
+import csv
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def from_db(path):
+    c = sqlite3.connect(path)
+    rows = c.execute("select name, duration from kernels").fetchall()
+    return rows
+
+
+def from_csv(path):
+    rows = []
+    with open(path) as f:
+        r = csv.DictReader(f)
+        for d in r:
+            name = d.get("Kernel_Name") or d.get("KernelName") or d.get("Name")
+            if "Start_Timestamp" in d:
+                dur = int(d["End_Timestamp"]) - int(d["Start_Timestamp"])
+            else:
+                dur = int(float(d.get("DurationNs") or d.get("duration")))
+            rows.append((name, dur))
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("--out")
+    ap.add_argument("--title", default="rocprofv3 --kernel-trace summary")
+    a = ap.parse_args()
+    rows = from_db(a.src) if a.src.endswith(".db") else from_csv(a.src)
+    agg = defaultdict(list)
+    for name, dur in rows:
+        agg[name].append(dur)
+    total = sum(sum(v) for v in agg.values())
+    lines = [f"# {a.title}", "", f"source: `{a.src}`", "",
+             "| kernel | calls | total ms | avg µs | min µs | max µs | share |",
+             "|---|---:|---:|---:|---:|---:|---:|"]
+    for name, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
+        s = sum(v)
+        nm = name.replace("|", "\\|")
+        if len(nm) > 110:
+            nm = nm[:107] + "..."
+        lines.append(f"| `{nm}` | {len(v)} | {s / 1e6:.3f} | {s / len(v) / 1e3:.1f} | {min(v) / 1e3:.1f} | "
+                     f"{max(v) / 1e3:.1f} | {100.0 * s / max(total, 1):.1f}% |")
+    text = "\n".join(lines) + "\n"
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(text)
+    sys.stdout.write(text)
+
+
+if __name__ == "__main__":
+    main()
