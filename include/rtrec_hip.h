@@ -146,6 +146,7 @@ typedef struct {
     double* stats_out;       /* [2n] accumulated (NULL = skip)                         */
     float* l2_out;           /* [m, n] normalized rows (final layer) or NULL          */
     float* norms_out;        /* [m] row norms (with l2_out)                            */
+    int64_t* num_batches_tracked; /* prev BN counter, +1 by block 0 in mode 1 (may be NULL) */
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
@@ -233,7 +234,9 @@ int rt_similarity_f32(const float* u, const float* v, int64_t b, int d, float in
  * Optimiser (src/training/trainers/two_tower.py:60-64,144) on ONE flat fp32
  * parameter slab (all tower tensors + biases contiguous) and its grad slab:
  * rt_grad_sqnorm: sumsq_out[t] += Σ g² over tensor t = [offsets[t], offsets[t+1])
- *   (offsets: device int64 [n_tensors+1]; sumsq_out fp64, caller zeroes).
+ *   (offsets: device int64 [n_tensors+1]; sumsq_out fp64, caller zeroes); also
+ *   increments the device step / dropout-seed counters when non-NULL (one
+ *   thread), so a replayed hipGraph advances them without extra launches.
  * rt_clip_adam_step: clip_grad_norm_(max_norm): coef = min(1, max_norm /
  *   (sqrt(Σ_t sumsq[t]) + 1e-6)); then torch.optim.Adam with L2 weight decay and
  *   bias correction on g·coef. The step count and learning rate are read from
@@ -241,7 +244,7 @@ int rt_similarity_f32(const float* u, const float* v, int64_t b, int d, float in
  *   from `step` / `lr`.
  * ------------------------------------------------------------------------ */
 int rt_grad_sqnorm(const float* grads, const int64_t* offsets, int n_tensors, double* sumsq_out,
-                   void* stream);
+                   int32_t* step_counter, int64_t* seed_counter, void* stream);
 int rt_clip_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                       int64_t n, const double* sumsq, int n_tensors, float max_norm, float lr,
                       const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,

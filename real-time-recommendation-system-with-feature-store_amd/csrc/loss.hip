@@ -26,6 +26,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int RB = 32;        // users (or items) per block
 constexpr int kMaxD = 256;
 constexpr int kMaxNeg = 64;
+constexpr int NG = 16;  // negatives reduced together
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -43,7 +44,23 @@ __device__ __forceinline__ f32x16 dot_tile(const float* __restrict__ A, int64_t 
     const float* pa = A + ar * D + h * (D / 2);
     const float* pb = Bm + br * D + h * (D / 2);
     f32x16 acc = {};
-    for (int s = 0; s < D / 2; s += 4) {
+    int s = 0;
+    for (; s + 16 <= D / 2; s += 16) {  // 8 independent 16-byte loads in flight
+        float4 av[4], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            av[j] = *reinterpret_cast<const float4*>(pa + s + 4 * j);
+            bv[j] = *reinterpret_cast<const float4*>(pb + s + 4 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc = mfma(av[j].x, bv[j].x, acc);
+            acc = mfma(av[j].y, bv[j].y, acc);
+            acc = mfma(av[j].z, bv[j].z, acc);
+            acc = mfma(av[j].w, bv[j].w, acc);
+        }
+    }
+    for (; s < D / 2; s += 4) {
         const float4 av = *reinterpret_cast<const float4*>(pa + s);
         const float4 bv = *reinterpret_cast<const float4*>(pb + s);
         acc = mfma(av.x, bv.x, acc);
@@ -58,30 +75,66 @@ struct Args {
     const float* u; const float* p; const float* q;
     int64_t b; int d; int n_neg; float inv_tau;
     const float* ub; const float* ib;
-    float we, wb;
+    float we, wb;       // weights of the explicit / in-batch terms in loss_out[0]
     double* loss;
     float* du; float* dp; float* dq; float* dub; float* dib;
-    float* lse;  // workspace [b]
+    float2* part;       // workspace [n_split][b]: per-split (max, sum exp) of S rows
+    float* diag;        // workspace [b]: S_ii = u_i·p_i / tau
+    int n_split;        // item splits of 128 (JT) per user tile
     bool grad;
 };
 
+constexpr int JT = 128;  // streamed rows per block (4 waves x 32)
+
 // ---------------------------------------------------------------- launch 1
-__global__ __launch_bounds__(256) void loss_rows_kernel(Args a) {
-    __shared__ float diag[RB];
+// block (it, js): in-batch partial row log-sum-exp of users [32it, 32it+32) over
+// items [128js, 128js+128) (one 32x32 S^T tile per wave), plus the explicit
+// contrastive CE of a strided subset of the tile's users (one wave per user).
+__global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
     __shared__ float negs[4][kMaxNeg];
     __shared__ float red_m[4][RB], red_l[4][RB];
-    __shared__ double red_loss[4][2];
-    __shared__ float red_bias[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
-    const int64_t i0 = static_cast<int64_t>(blockIdx.x) * RB;
+    const int it = blockIdx.x, js = blockIdx.y;
+    const int64_t i0 = static_cast<int64_t>(it) * RB;
     const int D = a.d;
     const float bias = (a.ub ? a.ub[0] : 0.f) + (a.ib ? a.ib[0] : 0.f);
     const float inv_b = 1.f / static_cast<float>(a.b);
+
+    // ---- in-batch partial lse: S^T tile (items j × users i) ----
+    {
+        const int64_t t = static_cast<int64_t>(js) * 4 + w;   // item tile of this wave
+        float om = -INFINITY, ol = 0.f;
+        if (t * 32 < a.b) {
+            const f32x16 acc = dot_tile(a.p, t * 32, a.b, a.u, i0, a.b, D);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t j = t * 32 + tile_row(r, h);
+                if (j < a.b) {
+                    const float sv = acc[r] * a.inv_tau;
+                    if (sv > om) { ol = ol * expf(om - sv) + 1.f; om = sv; }
+                    else ol += expf(sv - om);
+                }
+            }
+        }
+        const float m2 = __shfl_xor(om, 32, 64), l2 = __shfl_xor(ol, 32, 64);
+        const float mm = fmaxf(om, m2);
+        ol = (mm == -INFINITY) ? 0.f : ol * expf(om - mm) + l2 * expf(m2 - mm);
+        if (h == 0) { red_m[w][c] = mm; red_l[w][c] = ol; }
+    }
+    __syncthreads();
+    if (w == 0 && h == 0 && i0 + c < a.b) {
+        float mm = -INFINITY;
+        for (int x = 0; x < 4; ++x) mm = fmaxf(mm, red_m[x][c]);
+        float ll = 0.f;
+        if (mm != -INFINITY)
+            for (int x = 0; x < 4; ++x) ll += red_l[x][c] * expf(red_m[x][c] - mm);
+        a.part[static_cast<int64_t>(js) * a.b + i0 + c] = make_float2(mm, ll);
+    }
+
+    // ---- explicit negatives: users ii = 4js + w, stepping 4*n_split ----
     double loss_e = 0.0;
     float dbias_acc = 0.f;
-
-    // ---- explicit negatives: one wave per user, lanes over d ----
-    for (int ii = w * 8; ii < w * 8 + 8; ++ii) {
+    for (int ii = js * 4 + w; ii < RB; ii += 4 * a.n_split) {
         const int64_t i = i0 + ii;
         if (i >= a.b) break;
         const float* ur = a.u + i * D;
@@ -96,7 +149,7 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(Args a) {
             part += uv[t] * pv[t];
         }
         const float dup = wave_sum(part) * a.inv_tau;
-        if (lane == 0) diag[ii] = dup;
+        if (lane == 0) a.diag[i] = dup;
         if (a.n_neg <= 0) {
             if (a.grad) {
 #pragma unroll
@@ -108,163 +161,179 @@ __global__ __launch_bounds__(256) void loss_rows_kernel(Args a) {
             continue;
         }
         const float pos = dup + bias;
+        // all negative dots of a group of 16 at once: independent loads, one
+        // butterfly reduction for the 16 partial sums
         float mx = pos;
-        for (int j = 0; j < a.n_neg; ++j) {
-            const float* qr = a.q + (i * a.n_neg + j) * D;
-            float pq = 0.f;
+        for (int g0 = 0; g0 < a.n_neg; g0 += NG) {
+            float part_j[NG];
 #pragma unroll
-            for (int t = 0; t < kMaxD / 64; ++t) {
-                const int dd = lane + 64 * t;
-                if (dd < D) pq += uv[t] * qr[dd];
+            for (int jj = 0; jj < NG; ++jj) {
+                part_j[jj] = 0.f;
+                const int j = g0 + jj;
+                if (j < a.n_neg) {
+                    const float* qr = a.q + (i * a.n_neg + j) * D;
+#pragma unroll
+                    for (int t = 0; t < kMaxD / 64; ++t) {
+                        const int dd = lane + 64 * t;
+                        if (dd < D) part_j[jj] += uv[t] * qr[dd];
+                    }
+                }
             }
-            const float nv = wave_sum(pq) * a.inv_tau;
-            if (lane == 0) negs[w][j] = nv;
-            mx = fmaxf(mx, nv);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+                for (int jj = 0; jj < NG; ++jj) part_j[jj] += __shfl_xor(part_j[jj], o, 64);
+#pragma unroll
+            for (int jj = 0; jj < NG; ++jj) {
+                if (g0 + jj < a.n_neg) {
+                    const float nv = part_j[jj] * a.inv_tau;
+                    if (lane == 0) negs[w][g0 + jj] = nv;
+                    mx = fmaxf(mx, nv);
+                }
+            }
         }
         wave_lds_sync();
         float se = expf(pos - mx);
         for (int j = 0; j < a.n_neg; ++j) se += expf(negs[w][j] - mx);
         const float lse = mx + logf(se);
         if (lane == 0) loss_e += static_cast<double>(lse - pos);
-        if (!a.grad) continue;
-        const float dpos = a.we * inv_b * (expf(pos - lse) - 1.f);
-        if (lane == 0) dbias_acc += dpos;
-        float duv[kMaxD / 64];
+        if (a.grad) {
+            const float dpos = a.we * inv_b * (expf(pos - lse) - 1.f);
+            if (lane == 0) dbias_acc += dpos;
+            float duv[kMaxD / 64];
 #pragma unroll
-        for (int t = 0; t < kMaxD / 64; ++t) duv[t] = dpos * pv[t];
-        for (int j = 0; j < a.n_neg; ++j) {
-            const float dn = a.we * inv_b * expf(negs[w][j] - lse);
-            const float* qr = a.q + (i * a.n_neg + j) * D;
-            float* dqr = a.dq + (i * a.n_neg + j) * D;
+            for (int t = 0; t < kMaxD / 64; ++t) duv[t] = dpos * pv[t];
+            for (int g0 = 0; g0 < a.n_neg; g0 += NG) {
+                float qv[NG][kMaxD / 64];
+#pragma unroll
+                for (int jj = 0; jj < NG; ++jj) {
+                    const int j = g0 + jj;
+                    const float* qr = a.q + (i * a.n_neg + (j < a.n_neg ? j : 0)) * D;
+#pragma unroll
+                    for (int t = 0; t < kMaxD / 64; ++t) {
+                        const int dd = lane + 64 * t;
+                        qv[jj][t] = (j < a.n_neg && dd < D) ? qr[dd] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int jj = 0; jj < NG; ++jj) {
+                    const int j = g0 + jj;
+                    if (j >= a.n_neg) break;
+                    const float dn = a.we * inv_b * expf(negs[w][j] - lse);
+                    float* dqr = a.dq + (i * a.n_neg + j) * D;
+#pragma unroll
+                    for (int t = 0; t < kMaxD / 64; ++t) {
+                        const int dd = lane + 64 * t;
+                        if (dd < D) {
+                            duv[t] += dn * qv[jj][t];
+                            dqr[dd] = dn * uv[t] * a.inv_tau;
+                        }
+                    }
+                }
+            }
 #pragma unroll
             for (int t = 0; t < kMaxD / 64; ++t) {
                 const int dd = lane + 64 * t;
                 if (dd < D) {
-                    duv[t] += dn * qr[dd];
-                    dqr[dd] = dn * uv[t] * a.inv_tau;
+                    a.du[i * D + dd] = duv[t] * a.inv_tau;
+                    a.dp[i * D + dd] = dpos * uv[t] * a.inv_tau;
                 }
             }
         }
-#pragma unroll
-        for (int t = 0; t < kMaxD / 64; ++t) {
-            const int dd = lane + 64 * t;
-            if (dd < D) {
-                a.du[i * D + dd] = duv[t] * a.inv_tau;
-                a.dp[i * D + dd] = dpos * uv[t] * a.inv_tau;
-            }
-        }
+        wave_lds_sync();
     }
-    __syncthreads();
-
-    // ---- in-batch row log-sum-exp: S^T tiles [32 items j × 32 users i] ----
-    float om = -INFINITY, ol = 0.f;
-    const int64_t ntiles = (a.b + 31) / 32;
-    for (int64_t t = w; t < ntiles; t += 4) {
-        const f32x16 acc = dot_tile(a.p, t * 32, a.b, a.u, i0, a.b, D);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int64_t j = t * 32 + tile_row(r, h);
-            if (j < a.b) {
-                const float s = acc[r] * a.inv_tau;
-                if (s > om) { ol = ol * expf(om - s) + 1.f; om = s; }
-                else ol += expf(s - om);
-            }
-        }
+    if (lane == 0 && loss_e != 0.0) {
+        const double le = loss_e / static_cast<double>(a.b);
+        atomicAdd(&a.loss[1], le);
+        atomicAdd(&a.loss[0], a.we * le);
     }
-    {   // merge the two half-waves (same user column)
-        const float m2 = __shfl_xor(om, 32, 64), l2 = __shfl_xor(ol, 32, 64);
-        const float mm = fmaxf(om, m2);
-        ol = (mm == -INFINITY) ? 0.f : ol * expf(om - mm) + l2 * expf(m2 - mm);
-        om = mm;
-    }
-    if (h == 0) { red_m[w][c] = om; red_l[w][c] = ol; }
-    __syncthreads();
-    double loss_b = 0.0;
-    if (w == 0 && h == 0) {
-        float mm = -INFINITY;
-        for (int x = 0; x < 4; ++x) mm = fmaxf(mm, red_m[x][c]);
-        float ll = 0.f;
-        for (int x = 0; x < 4; ++x)
-            if (red_m[x][c] != -INFINITY) ll += red_l[x][c] * expf(red_m[x][c] - mm);
-        const int64_t i = i0 + c;
-        if (i < a.b) {
-            const float lse = mm + logf(ll);
-            a.lse[i] = lse;
-            loss_b = static_cast<double>(lse - diag[c]);
-        }
-    }
-    // ---- block reduction of the losses / bias grad ----
-    loss_e = wave_sum(loss_e);
-    loss_b = wave_sum(loss_b);
-    const float db = wave_sum(dbias_acc);
-    if (lane == 0) { red_loss[w][0] = loss_e; red_loss[w][1] = loss_b; red_bias[w] = db; }
-    __syncthreads();
-    if (tid == 0) {
-        double le = 0.0, lb = 0.0;
-        float dbs = 0.f;
-        for (int x = 0; x < 4; ++x) { le += red_loss[x][0]; lb += red_loss[x][1]; dbs += red_bias[x]; }
-        const double inv_bd = 1.0 / static_cast<double>(a.b);
-        atomicAdd(&a.loss[1], le * inv_bd);
-        atomicAdd(&a.loss[2], lb * inv_bd);
-        atomicAdd(&a.loss[0], (a.n_neg > 0 ? a.we * le * inv_bd : 0.0) + (a.n_neg > 0 ? a.wb : 1.f) * lb * inv_bd);
-        if (a.grad && a.n_neg > 0) {
-            if (a.dub) atomicAdd(a.dub, dbs);
-            if (a.dib) atomicAdd(a.dib, dbs);
-        }
+    if (lane == 0 && a.grad && a.n_neg > 0 && dbias_acc != 0.f) {
+        if (a.dub) atomicAdd(a.dub, dbias_acc);
+        if (a.dib) atomicAdd(a.dib, dbias_acc);
     }
 }
 
+// combine the per-split partials of user i into its log-sum-exp
+__device__ __forceinline__ float combine_lse(const float2* part, int n_split, int64_t b, int64_t i) {
+    float mm = -INFINITY;
+    for (int s = 0; s < n_split; ++s) mm = fmaxf(mm, part[static_cast<int64_t>(s) * b + i].x);
+    float ll = 0.f;
+    for (int s = 0; s < n_split; ++s) {
+        const float2 v = part[static_cast<int64_t>(s) * b + i];
+        if (v.x != -INFINITY) ll += v.y * expf(v.x - mm);
+    }
+    return mm + logf(ll);
+}
+
 // ---------------------------------------------------------------- launch 2
+// blockIdx.z = 0: row pass, fixed 32 users, dU += dS · P over 128 streamed items
+// blockIdx.z = 1: column pass, fixed 32 items, dP += dSᵀ · U over 128 streamed users
+// (dS = wb/B·(softmax(S) − I)); results added atomically (n_split adds per element).
 template <int DT>  // D/32 output tiles per wave accumulator
-__global__ __launch_bounds__(256) void loss_inbatch_bwd_kernel(Args a, float wb_eff) {
+__global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, bool add_loss) {
     __shared__ float Ds[4][32][33];
+    __shared__ float lse_s[JT];       // row pass: [0,32) fixed users; column pass: 128 streamed users
     __shared__ float red[32 * (kMaxD + 1)];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
     const int D = a.d;
-    const int64_t nb = (a.b + 31) / 32;
-    const bool row_pass = blockIdx.x < nb;
-    const int64_t f0 = (row_pass ? blockIdx.x : blockIdx.x - nb) * static_cast<int64_t>(RB);  // fixed 32 rows
-    const float* Str = row_pass ? a.p : a.u;      // streamed operand
+    const bool row_pass = blockIdx.z == 0;
+    const int64_t f0 = static_cast<int64_t>(blockIdx.x) * RB;      // fixed tile
+    const int64_t s0 = static_cast<int64_t>(blockIdx.y) * JT;      // streamed range
+    const float* Str = row_pass ? a.p : a.u;
     const float scale = wb_eff / static_cast<float>(a.b);
+    if (row_pass) {
+        if (tid < RB) {
+            const int64_t i = f0 + tid;
+            const float l = i < a.b ? combine_lse(a.part, a.n_split, a.b, i) : 0.f;
+            lse_s[tid] = l;
+            if (add_loss && blockIdx.y == 0 && i < a.b) {
+                const double li = static_cast<double>(l - a.diag[i]) / static_cast<double>(a.b);
+                atomicAdd(&a.loss[2], li);
+                atomicAdd(&a.loss[0], static_cast<double>(wb_eff) * li);
+            }
+        }
+    } else if (tid < JT) {
+        const int64_t i = s0 + tid;
+        lse_s[tid] = i < a.b ? combine_lse(a.part, a.n_split, a.b, i) : 0.f;
+    }
+    for (int e = tid; e < 32 * (kMaxD + 1); e += 256) red[e] = 0.f;
+    __syncthreads();
+    if (!a.grad) return;
     f32x16 acc[DT];
 #pragma unroll
     for (int x = 0; x < DT; ++x) acc[x] = f32x16{};
-    // row pass: tile element (row = item j, col = user i) → lse of the user = lane's column
-    const float lse_col = (row_pass && f0 + c < a.b) ? a.lse[f0 + c] : 0.f;
-    const int64_t ntiles = nb;
-    for (int64_t t = w; t < ntiles; t += 4) {
-        const f32x16 st = row_pass ? dot_tile(a.p, t * 32, a.b, a.u, f0, a.b, D)    // (j, i)
-                                   : dot_tile(a.u, t * 32, a.b, a.p, f0, a.b, D);   // (i, j)
+    const int64_t t0 = s0 + w * 32;  // this wave's streamed tile
+    if (t0 < a.b) {
+        // row pass: (row = item j, col = user i);  column pass: (row = user i, col = item j)
+        const f32x16 st = row_pass ? dot_tile(a.p, t0, a.b, a.u, f0, a.b, D)
+                                   : dot_tile(a.u, t0, a.b, a.p, f0, a.b, D);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int rr = tile_row(r, h);
-            const int64_t srow = t * 32 + rr;   // streamed index
-            const int64_t fcol = f0 + c;        // fixed index
+            const int64_t srow = t0 + rr;
+            const int64_t fcol = f0 + c;
             float ds = 0.f;
             if (srow < a.b && fcol < a.b) {
-                const float lse = row_pass ? lse_col : a.lse[srow];
+                const float lse = row_pass ? lse_s[c] : lse_s[w * 32 + rr];
                 const float pr = expf(st[r] * a.inv_tau - lse);
                 ds = scale * (pr - (srow == fcol ? 1.f : 0.f));
             }
             Ds[w][c][rr] = ds;  // [fixed][streamed]
         }
         wave_lds_sync();
-        // acc[dt] (fixed f × d) += Σ_s Ds[f][s] · Str[t*32 + s][d]
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
             const int dcol = dt * 32 + c;
+#pragma unroll 4
             for (int s = 0; s < 16; ++s) {
                 const int ks = 2 * s + h;
-                const int64_t sr = t * 32 + ks;
+                const int64_t sr = t0 + ks;
                 const float bv = (sr < a.b && dcol < D) ? Str[sr * D + dcol] : 0.f;
                 acc[dt] = mfma(Ds[w][c][ks], bv, acc[dt]);
             }
         }
-        wave_lds_sync();
     }
-    // reduce the 4 wave partials through LDS: red[f][d]
-    for (int e = tid; e < 32 * (kMaxD + 1); e += 256) red[e] = 0.f;
-    __syncthreads();
+    // reduce the 4 wave partials through LDS (red[fixed][d]), then atomically add
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -274,7 +343,7 @@ __global__ __launch_bounds__(256) void loss_inbatch_bwd_kernel(Args a, float wb_
     for (int e = tid; e < 32 * D; e += 256) {
         const int f = e / D, dd = e % D;
         const int64_t gi = f0 + f;
-        if (gi < a.b) out[gi * D + dd] += red[f * (kMaxD + 1) + dd] * a.inv_tau;
+        if (gi < a.b) atomicAdd(&out[gi * D + dd], red[f * (kMaxD + 1) + dd] * a.inv_tau);
     }
 }
 
@@ -309,34 +378,45 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
     if (d % 8 != 0 || d > loss::kMaxD || n_neg > loss::kMaxNeg) return RT_ERR_UNSUPPORTED;
     if (n_neg > 0 && !q) return RT_ERR_INVALID;
     if (grad && (!du || !dp || (n_neg > 0 && !dq))) return RT_ERR_INVALID;
-    if (!ws || ws_bytes < static_cast<size_t>(b) * sizeof(float)) return RT_ERR_WORKSPACE;
+    const int n_split = static_cast<int>((b + loss::JT - 1) / loss::JT);
+    const size_t need = static_cast<size_t>(n_split) * b * sizeof(float2) + static_cast<size_t>(b) * sizeof(float);
+    if (!ws || ws_bytes < need) return RT_ERR_WORKSPACE;
     if ((reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(p)) & 15) return RT_ERR_INVALID;
+    float2* part = reinterpret_cast<float2*>(ws);
+    float* diag = reinterpret_cast<float*>(part + static_cast<size_t>(n_split) * b);
+    const float wb_eff = n_neg > 0 ? wb : 1.f;  // in-batch alone: the loss IS the in-batch CE (weight 1)
+    const float we_eff = n_neg > 0 ? we : 0.f;
     loss::Args a{static_cast<const float*>(u), static_cast<const float*>(p), static_cast<const float*>(q),
-                 b, d, n_neg, inv_tau, ub, ib, we, wb, loss_out, du, dp, dq, dub, dib,
-                 static_cast<float*>(ws), grad};
+                 b, d, n_neg, inv_tau, ub, ib, we_eff, wb_eff, loss_out, du, dp, dq, dub, dib, part, diag,
+                 n_split, grad};
     hipStream_t st = as_stream(stream);
-    const unsigned nb = static_cast<unsigned>((b + loss::RB - 1) / loss::RB);
-    hipLaunchKernelGGL(loss::loss_rows_kernel, dim3(nb), dim3(256), 0, st, a);
-    int rc = check_launch("loss_rows_kernel");
-    if (rc || !grad) return rc;
-    const float wb_eff = n_neg > 0 ? wb : 1.f;  // in-batch only: the loss IS the in-batch CE
-    if (wb_eff == 0.f) return RT_OK;            // contrastive_loss alone
+    const unsigned nt = static_cast<unsigned>((b + loss::RB - 1) / loss::RB);
+    hipLaunchKernelGGL(loss::loss_fwd_kernel, dim3(nt, n_split), dim3(256), 0, st, a);
+    int rc = check_launch("loss_fwd_kernel");
+    if (rc) return rc;
+    const bool want_ib = wb_eff != 0.f;
+    if (!want_ib) return RT_OK;  // contrastive_loss alone
+    // forward-only calls still need launch 2's row pass for the in-batch loss value
+    const dim3 grid(nt, n_split, grad ? 2 : 1);
     const int dt = (d + 31) / 32;
     switch (dt) {
-        case 1: hipLaunchKernelGGL(loss::loss_inbatch_bwd_kernel<1>, dim3(2 * nb), dim3(256), 0, st, a, wb_eff); break;
-        case 2: hipLaunchKernelGGL(loss::loss_inbatch_bwd_kernel<2>, dim3(2 * nb), dim3(256), 0, st, a, wb_eff); break;
+        case 1: hipLaunchKernelGGL(loss::loss_bwd_kernel<1>, grid, dim3(256), 0, st, a, wb_eff, true); break;
+        case 2: hipLaunchKernelGGL(loss::loss_bwd_kernel<2>, grid, dim3(256), 0, st, a, wb_eff, true); break;
         case 3:
-        case 4: hipLaunchKernelGGL(loss::loss_inbatch_bwd_kernel<4>, dim3(2 * nb), dim3(256), 0, st, a, wb_eff); break;
-        default: hipLaunchKernelGGL(loss::loss_inbatch_bwd_kernel<8>, dim3(2 * nb), dim3(256), 0, st, a, wb_eff); break;
+        case 4: hipLaunchKernelGGL(loss::loss_bwd_kernel<4>, grid, dim3(256), 0, st, a, wb_eff, true); break;
+        default: hipLaunchKernelGGL(loss::loss_bwd_kernel<8>, grid, dim3(256), 0, st, a, wb_eff, true); break;
     }
-    return check_launch("loss_inbatch_bwd_kernel");
+    return check_launch("loss_bwd_kernel");
 }
 }  // namespace
 
 extern "C" size_t rt_twotower_loss_workspace_bytes(int64_t b, int d) {
     (void)d;
-    return static_cast<size_t>(b > 0 ? b : 1) * sizeof(float) + 256;
+    if (b <= 0) return 256;
+    const int64_t n_split = (b + loss::JT - 1) / loss::JT;
+    return static_cast<size_t>(n_split) * b * sizeof(float2) + static_cast<size_t>(b) * sizeof(float) + 256;
 }
+
 
 extern "C" int rt_twotower_loss_fwd_bwd(const void* u, const void* p, const void* q, int dtype, int64_t b, int d,
                                         int n_neg, float inv_tau, const float* user_bias, const float* item_bias,

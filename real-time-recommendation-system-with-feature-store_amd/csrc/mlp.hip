@@ -20,9 +20,8 @@ namespace mlp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BM = 64;        // rows per block (forward, backward-1)
-constexpr int KC = 32;        // reduction chunk staged in LDS
-constexpr int LDK = KC + 1;   // odd stride: conflict-free ds_read_b32 fragment reads
+
+
 constexpr float kNormEps = 1e-12f;
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
@@ -57,24 +56,31 @@ __device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, f
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
-template <int TPW>  // 32x32 output tiles per wave; padded width NP = 64*TPW
+// Block = 32 rows x all n columns; the transformed A tile (32 x k) lives in LDS
+// for the whole reduction (A fragments by ds_read_b128), W fragments stream
+// straight from L2 (float4 per lane per 4 MFMAs). The reduction index is
+// permuted (lane half h covers k in [h*kh, h*kh+kh)) so each lane's operands
+// are contiguous; 4 waves split the output columns.
+constexpr int FM = 32;  // rows per block
+
+__host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // kh % 16 == 0
+
+template <int TPW, bool KVEC>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
 __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
-    constexpr int NP = 64 * TPW;
+    constexpr int NT = 4 * TPW;  // column tiles in the block
     extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int kpad = (a.k + KC - 1) / KC * KC;
-    float* scale = sm;                       // [kpad]
-    float* shift = scale + kpad;             // [kpad]
-    float* As = shift + kpad;                // [BM][LDK]
-    float* Ws = As + BM * LDK;               // [NP][LDK]
-    float* rowpart = Ws + NP * LDK;          // [NP/32][BM] per column-tile row sums (l2)
-    int64_t* srow = reinterpret_cast<int64_t*>(rowpart + (NP / 32) * BM);  // [BM]
+    const int k = a.k, n = a.n;
+    const int kp = pad8(k), kh = kp / 2, lda = kp + 4;
+    float* scale = sm;                   // [kp]
+    float* shift = scale + kp;           // [kp]
+    float* As = shift + kp;              // [FM][lda]
+    float* rowpart = As + FM * lda;      // [NT][FM]
+    int64_t* srow = reinterpret_cast<int64_t*>(rowpart + NT * FM);  // [FM]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
-    const int k = a.k, n = a.n;
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * FM;
     const int64_t m = a.m;
 
-    // ---- prologue setup: BatchNorm affine of the previous block ----
     if (a.prev_mode == 1 || a.prev_mode == 2) {
         for (int c = tid; c < k; c += 256) {
             float mean, invstd, var_f = 0.f;
@@ -91,6 +97,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
             }
             bn_affine(a.bn_gamma[c], a.bn_beta[c], mean, invstd, scale[c], shift[c]);
             if (blockIdx.x == 0) {
+                if (c == 0 && a.prev_mode == 1 && a.num_batches_tracked) *a.num_batches_tracked += 1;
                 if (a.save_mean) a.save_mean[c] = mean;
                 if (a.save_invstd) a.save_invstd[c] = invstd;
                 if (a.prev_mode == 1 && a.running_mean) {
@@ -101,47 +108,110 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
             }
         }
     }
-    for (int r = tid; r < BM; r += 256) {
-        const int64_t gr = row0 + r;
+    if (tid < FM) {
+        const int64_t gr = row0 + tid;
         int64_t sr = -1;
         if (gr < m) {
             sr = a.ids ? a.ids[gr] : gr;
             if (sr < 0 || sr >= a.src_rows) sr = -1;
         }
-        srow[r] = sr;
+        srow[tid] = sr;
     }
+    __syncthreads();
     const uint64_t seed = a.drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.drop_p, a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f, seed,
                   scale, shift};
+    {   // stage the transformed A tile: float4 loads, 4 in flight per thread
+        const int vpr = kp / 4;
+        const int total = FM * vpr;
+        const bool vec = (a.ld_src % 4) == 0 && (reinterpret_cast<uintptr_t>(a.src) & 15) == 0;
+        for (int base = tid; base < total; base += 256 * 4) {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = base + u * 256;
+                v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (e < total) {
+                    const int r = e / vpr, c = (e - r * vpr) * 4;
+                    const int64_t sr = srow[r];
+                    if (sr >= 0 && c < k) {
+                        const float* sp = a.src + sr * a.ld_src + c;
+                        if (vec && c + 4 <= k) v[u] = *reinterpret_cast<const float4*>(sp);
+                        else {
+                            v[u].x = sp[0];
+                            if (c + 1 < k) v[u].y = sp[1];
+                            if (c + 2 < k) v[u].z = sp[2];
+                            if (c + 3 < k) v[u].w = sp[3];
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = base + u * 256;
+                if (e < total) {
+                    const int r = e / vpr, c = (e - r * vpr) * 4;
+                    const bool ok = srow[r] >= 0;
+                    const int64_t gr = row0 + r;
+                    float4 o;
+                    o.x = (ok && c < k) ? pro_apply(pro, gr, c, v[u].x) : 0.f;
+                    o.y = (ok && c + 1 < k) ? pro_apply(pro, gr, c + 1, v[u].y) : 0.f;
+                    o.z = (ok && c + 2 < k) ? pro_apply(pro, gr, c + 2, v[u].z) : 0.f;
+                    o.w = (ok && c + 3 < k) ? pro_apply(pro, gr, c + 3, v[u].w) : 0.f;
+                    *reinterpret_cast<float4*>(As + r * lda + c) = o;
+                }
+            }
+        }
+    }
+    __syncthreads();
 
     f32x16 acc[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) acc[i] = f32x16{};
-    const int rt = w & 1;
-    for (int k0 = 0; k0 < k; k0 += KC) {
-        __syncthreads();
-        for (int e = tid; e < BM * KC; e += 256) {
-            const int r = e / KC, c = e % KC;
-            const int gc = k0 + c;
-            float v = 0.f;
-            const int64_t sr = srow[r];
-            if (sr >= 0 && gc < k) v = pro_apply(pro, row0 + r, gc, a.src[sr * a.ld_src + gc]);
-            As[r * LDK + c] = v;
-        }
-        for (int e = tid; e < NP * KC; e += 256) {
-            const int nn = e / KC, c = e % KC;
-            const int gc = k0 + c;
-            Ws[nn * LDK + c] = (nn < n && gc < k) ? a.w[static_cast<int64_t>(nn) * k + gc] : 0.f;
-        }
-        __syncthreads();
-        const float* ap = As + (rt * 32 + c32) * LDK + h;
-#pragma unroll 4
-        for (int s = 0; s < KC / 2; ++s) {
-            const float av = ap[2 * s];
+    const float* ap = As + c32 * lda + h * kh;
+    const float* wrow[TPW];
+    bool tile_on[TPW], row_ok[TPW];
 #pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                const int ct = (w >> 1) + 2 * i;
-                acc[i] = mfma(av, Ws[(ct * 32 + c32) * LDK + 2 * s + h], acc[i]);
+    for (int i = 0; i < TPW; ++i) {
+        tile_on[i] = (w + 4 * i) * 32 < n;  // wave-uniform
+        const int nn = (w + 4 * i) * 32 + c32;
+        row_ok[i] = nn < n;
+        wrow[i] = a.w + static_cast<int64_t>(row_ok[i] ? nn : 0) * k;
+    }
+    // 16 k-steps per iteration (kh % 16 == 0): all loads issued before the MFMAs
+    for (int s = 0; s < kh; s += 16) {
+        float4 av[4];
+        float4 wv[TPW][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) av[j] = *reinterpret_cast<const float4*>(ap + s + 4 * j);
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kk = h * kh + s + 4 * j;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (tile_on[i] && row_ok[i]) {
+                    const float* wr = wrow[i] + kk;
+                    if constexpr (KVEC) {
+                        if (kk < k) v = *reinterpret_cast<const float4*>(wr);
+                    } else {
+                        if (kk < k) v.x = wr[0];
+                        if (kk + 1 < k) v.y = wr[1];
+                        if (kk + 2 < k) v.z = wr[2];
+                        if (kk + 3 < k) v.w = wr[3];
+                    }
+                }
+                wv[i][j] = v;
+            }
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            if (!tile_on[i]) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[i] = mfma(av[j].x, wv[i][j].x, acc[i]);
+                acc[i] = mfma(av[j].y, wv[i][j].y, acc[i]);
+                acc[i] = mfma(av[j].z, wv[i][j].z, acc[i]);
+                acc[i] = mfma(av[j].w, wv[i][j].w, acc[i]);
             }
         }
     }
@@ -150,13 +220,14 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
     const bool l2 = a.l2_out != nullptr;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-        const int col = ((w >> 1) + 2 * i) * 32 + c32;
+        const int ct = w + 4 * i;
+        const int col = ct * 32 + c32;
         const bool col_ok = col < n;
         const float b = (col_ok && a.bias) ? a.bias[col] : 0.f;
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int lr = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
             const int64_t gr = row0 + lr;
             const float z = acc[i][r] + b;
             acc[i][r] = z;
@@ -171,7 +242,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
                 float q = ok ? z * z : 0.f;
 #pragma unroll
                 for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
-                if (c32 == 0) rowpart[((w >> 1) + 2 * i) * BM + lr] = q;
+                if (c32 == 0) rowpart[ct * FM + lr] = q;
             }
         }
         if (a.stats_out) {
@@ -185,16 +256,17 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
     }
     if (l2) {
         __syncthreads();
+        const int nt_used = (n + 31) / 32;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
-            const int col = ((w >> 1) + 2 * i) * 32 + c32;
+            const int col = (w + 4 * i) * 32 + c32;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int lr = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int64_t gr = row0 + lr;
                 if (gr < m && col < n) {
                     float ss = 0.f;
-                    for (int t = 0; t < NP / 32; ++t) ss += rowpart[t * BM + lr];  // fixed order
+                    for (int t = 0; t < nt_used; ++t) ss += rowpart[t * FM + lr];  // fixed order
                     const float nrm = sqrtf(ss);
                     a.l2_out[gr * n + col] = acc[i][r] / fmaxf(nrm, kNormEps);
                     if (col == 0 && a.norms_out) a.norms_out[gr] = nrm;
@@ -207,22 +279,21 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
 // ---------------------------------------------------------------------------
 // backward 1: dz, dbias, dgamma/dbeta, dA = dz·W (+ g_prev / dsrc epilogue)
 // ---------------------------------------------------------------------------
-template <int TPWK>  // dA output tiles per wave; padded k KP = 64*TPWK
+// Block = 32 rows. dz (32 x n) lives in LDS; dA = dz·W reads W[n][k] rows
+// coalesced along k straight from L2 (the reduction runs over n).
+template <int TPWK>  // 32-col dA tiles per wave (k <= 128*TPWK)
 __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a) {
-    constexpr int KP = 64 * TPWK;
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
-    const int npad = (n + KC - 1) / KC * KC;
-    const int ldz = npad + 1;
-    float* Dz = sm;                       // [BM][ldz]
-    float* Wt = Dz + BM * ldz;            // [KP][LDK]
+    const int np = pad8(n), nh = np / 2, ldz = np + 4;
+    float* Dz = sm;  // [FM][ldz]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * FM;
 
     // ---- phase A: dz tile ----
     if (a.grad_mode == 0) {
-        for (int rr = w * 16; rr < w * 16 + 16; ++rr) {
+        for (int rr = w * 8; rr < w * 8 + 8; ++rr) {
             const int64_t gr = row0 + rr;
             if (gr < m) {
                 float dot = 0.f;
@@ -231,7 +302,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
                 const float nrm = a.norms[gr];
                 const bool big = nrm > kNormEps;
                 const float inv = 1.f / (big ? nrm : kNormEps);
-                for (int c = lane; c < npad; c += 64) {
+                for (int c = lane; c < np; c += 64) {
                     float dz = 0.f;
                     if (c < n) {
                         const float dv = a.dout[gr * n + c];
@@ -241,41 +312,93 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
                     Dz[rr * ldz + c] = dz;
                 }
             } else {
-                for (int c = lane; c < npad; c += 64) Dz[rr * ldz + c] = 0.f;
+                for (int c = lane; c < np; c += 64) Dz[rr * ldz + c] = 0.f;
             }
         }
     } else {
+        // per-column BN-backward coefficients, then a float4 elementwise pass
+        float* cA = Dz + FM * ldz;   // γ·invstd (mode 1/2) or 1
+        float* cB = cA + np;         // Σg/m
+        float* cC = cB + np;         // Σg·x̂/m
+        float* cM = cC + np;         // mean
+        float* cI = cM + np;         // invstd
         const float inv_m = 1.f / static_cast<float>(m);
-        for (int e = tid; e < BM * npad; e += 256) {
-            const int r = e / npad, c = e % npad;
-            const int64_t gr = row0 + r;
-            float dz = 0.f;
-            if (gr < m && c < n) {
-                const float gv = a.g[gr * n + c];
-                const float zv = a.z[gr * n + c];
-                float dr;
+        for (int c = tid; c < np; c += 256) {
+            float A = 1.f, Bc = 0.f, C = 0.f, M = 0.f, I = 1.f;
+            if (c < n && (a.grad_mode == 1 || a.grad_mode == 2)) {
+                I = a.save_invstd[c];
+                M = a.save_mean[c];
+                A = a.bn_gamma[c] * I;
                 if (a.grad_mode == 1) {
-                    const float mean = a.save_mean[c], invstd = a.save_invstd[c];
-                    const float xh = (act_fwd(a.act, zv) - mean) * invstd;
-                    const float sg = static_cast<float>(a.g_stats[c]);
-                    const float sgx = static_cast<float>(a.g_stats[n + c]);
-                    dr = a.bn_gamma[c] * invstd * (gv - sg * inv_m - xh * sgx * inv_m);
-                } else if (a.grad_mode == 2) {
-                    dr = a.bn_gamma[c] * a.save_invstd[c] * gv;
-                } else {
-                    dr = gv;
+                    Bc = static_cast<float>(a.g_stats[c]) * inv_m;
+                    C = static_cast<float>(a.g_stats[n + c]) * inv_m;
                 }
-                dz = dr * act_bwd(a.act, zv);
-                a.dz_ws[gr * n + c] = dz;
             }
-            Dz[r * ldz + c] = dz;
+            cA[c] = A; cB[c] = Bc; cC[c] = C; cM[c] = M; cI[c] = I;
+        }
+        __syncthreads();
+        const int vpr = np / 4;
+        const int total = FM * vpr;
+        const bool vec = (n % 4) == 0;
+        for (int base = tid; base < total; base += 256 * 4) {
+            float4 gv[4], zv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = base + u * 256;
+                gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                zv[u] = gv[u];
+                if (e < total) {
+                    const int r = e / vpr, c = (e - r * vpr) * 4;
+                    const int64_t gr = row0 + r;
+                    if (gr < m && c < n) {
+                        const int64_t off = gr * n + c;
+                        if (vec) {
+                            gv[u] = *reinterpret_cast<const float4*>(a.g + off);
+                            zv[u] = *reinterpret_cast<const float4*>(a.z + off);
+                        } else {
+                            gv[u].x = a.g[off]; zv[u].x = a.z[off];
+                            if (c + 1 < n) { gv[u].y = a.g[off + 1]; zv[u].y = a.z[off + 1]; }
+                            if (c + 2 < n) { gv[u].z = a.g[off + 2]; zv[u].z = a.z[off + 2]; }
+                            if (c + 3 < n) { gv[u].w = a.g[off + 3]; zv[u].w = a.z[off + 3]; }
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int e = base + u * 256;
+                if (e >= total) continue;
+                const int r = e / vpr, c = (e - r * vpr) * 4;
+                const int64_t gr = row0 + r;
+                float dzv[4];
+                const float gs[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+                const float zs[4] = {zv[u].x, zv[u].y, zv[u].z, zv[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int cc = c + j;
+                    float dz = 0.f;
+                    if (gr < m && cc < n) {
+                        const float xh = (act_fwd(a.act, zs[j]) - cM[cc]) * cI[cc];
+                        const float dr = (a.grad_mode == 3) ? gs[j] : cA[cc] * (gs[j] - cB[cc] - xh * cC[cc]);
+                        dz = dr * act_bwd(a.act, zs[j]);
+                    }
+                    dzv[j] = dz;
+                }
+                *reinterpret_cast<float4*>(Dz + r * ldz + c) = make_float4(dzv[0], dzv[1], dzv[2], dzv[3]);
+                if (gr < m && c < n) {
+                    const int64_t off = gr * n + c;
+                    if (vec) *reinterpret_cast<float4*>(a.dz_ws + off) = make_float4(dzv[0], dzv[1], dzv[2], dzv[3]);
+                    else
+                        for (int j = 0; j < 4 && c + j < n; ++j) a.dz_ws[off + j] = dzv[j];
+                }
+            }
         }
     }
     __syncthreads();
     for (int c = tid; c < n; c += 256) {
         if (a.dbias) {
             float s = 0.f;
-            for (int r = 0; r < BM; ++r) s += Dz[r * ldz + c];
+            for (int r = 0; r < FM; ++r) s += Dz[r * ldz + c];
             atomicAdd(&a.dbias[c], s);
         }
         if (blockIdx.x == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
@@ -285,28 +408,37 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
     }
     if (!a.g_prev && !a.dsrc) return;
 
-    // ---- phase B: dA = dz · W  (reduction over n) ----
+    // ---- phase B: dA = dz · W  (reduction over n, permuted per lane half) ----
     f32x16 acc[TPWK];
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) acc[i] = f32x16{};
-    const int rt = w & 1;
-    for (int n0 = 0; n0 < npad; n0 += KC) {
-        __syncthreads();
-        for (int e = tid; e < KP * KC; e += 256) {
-            const int kk = e % KP, nn = e / KP;
-            const int gn = n0 + nn;
-            Wt[kk * LDK + nn] = (kk < k && gn < n) ? a.w[static_cast<int64_t>(gn) * k + kk] : 0.f;
-        }
-        __syncthreads();
-        const float* dp = Dz + (rt * 32 + c32) * ldz + n0 + h;
-#pragma unroll 4
-        for (int s = 0; s < KC / 2; ++s) {
-            const float av = dp[2 * s];
+    const float* dp = Dz + c32 * ldz + h * nh;
+    for (int s = 0; s < nh; s += 8) {  // 8 k-steps per iteration (nh % 16 == 0)
+        float4 av[2];
+        float wv[TPWK][8];
+        av[0] = *reinterpret_cast<const float4*>(dp + s);
+        av[1] = *reinterpret_cast<const float4*>(dp + s + 4);
 #pragma unroll
-            for (int i = 0; i < TPWK; ++i) {
-                const int ct = (w >> 1) + 2 * i;
-                acc[i] = mfma(av, Wt[(ct * 32 + c32) * LDK + 2 * s + h], acc[i]);
+        for (int i = 0; i < TPWK; ++i) {
+            const int kk = (w + 4 * i) * 32 + c32;
+            const bool on = (w + 4 * i) * 32 < k && kk < k;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int nn = h * nh + s + j;
+                wv[i][j] = (on && nn < n) ? a.w[static_cast<int64_t>(nn) * k + kk] : 0.f;
             }
+        }
+#pragma unroll
+        for (int i = 0; i < TPWK; ++i) {
+            if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
+            acc[i] = mfma(av[0].x, wv[i][0], acc[i]);
+            acc[i] = mfma(av[0].y, wv[i][1], acc[i]);
+            acc[i] = mfma(av[0].z, wv[i][2], acc[i]);
+            acc[i] = mfma(av[0].w, wv[i][3], acc[i]);
+            acc[i] = mfma(av[1].x, wv[i][4], acc[i]);
+            acc[i] = mfma(av[1].y, wv[i][5], acc[i]);
+            acc[i] = mfma(av[1].z, wv[i][6], acc[i]);
+            acc[i] = mfma(av[1].w, wv[i][7], acc[i]);
         }
     }
     const float pscale = a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f;
@@ -314,14 +446,14 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
-        const int kk = ((w >> 1) + 2 * i) * 32 + c32;
+        const int kk = (w + 4 * i) * 32 + c32;
         const bool col_ok = kk < k;
         float s1 = 0.f, s2 = 0.f;
         float pmean = 0.f, pinv = 0.f;
         if (want_stats && col_ok) { pmean = a.prev_mean[kk]; pinv = a.prev_invstd[kk]; }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int64_t gr = row0 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t gr = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
             if (gr < m && col_ok) {
                 const float da = acc[i][r];
                 if (a.dsrc) a.dsrc[gr * k + kk] = da;
@@ -352,15 +484,14 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
 // ---------------------------------------------------------------------------
 // backward 2: dW[n][k] += Σ_r dz[r][n] · A[r][k], M split over blockIdx.z
 // ---------------------------------------------------------------------------
-constexpr int DW_T = 64;   // output tile (n) x (k)
-constexpr int DW_R = 32;   // rows per staged chunk
-constexpr int DW_LD = DW_R + 1;
+constexpr int DW_T = 64;   // output tile (n) x (k); 4 waves of 32x32
 
+// No LDS: lane c of a wave reads dz[r][n0+c] and A[r][k0+c] for the rows of
+// its MFMA k-step (32 consecutive floats per half-wave = one coalesced line),
+// A recomputed by the forward prologue; 8 k-steps unrolled so 16 independent
+// loads are in flight per wave.
 __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a, int64_t rows_per_split) {
-    __shared__ float DzT[DW_T * DW_LD];
-    __shared__ float AT[DW_T * DW_LD];
     __shared__ float scale[DW_T], shift[DW_T];
-    __shared__ int64_t srow[DW_R];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
@@ -374,48 +505,54 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a
             else { scale[c] = 0.f; shift[c] = 0.f; }
         }
     }
-    // scale/shift are indexed by the global column inside pro_apply: offset the base
+    __syncthreads();
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
+    // scale/shift are indexed by the global column inside pro_apply: offset the base
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
                   pseed, scale - k0, shift - k0};
     const int wn = w & 1, wk = w >> 1;
+    const int gn = n0 + wn * 32 + c32;   // this lane's dz column (A operand row)
+    const int gk = k0 + wk * 32 + c32;   // this lane's A column (B operand column)
+    const bool n_ok = gn < n, k_ok = gk < k;
     f32x16 acc = f32x16{};
-    for (int64_t r0 = r_begin; r0 < r_end; r0 += DW_R) {
+    constexpr int U = 8;                 // k-steps per unrolled group (16 rows)
+    constexpr int CH = 256;              // rows whose source index is staged at a time
+    __shared__ int64_t srow_s[CH];
+    for (int64_t c0 = r_begin; c0 < r_end; c0 += CH) {
         __syncthreads();
-        if (tid < DW_R) {
-            const int64_t gr = r0 + tid;
+        for (int t = tid; t < CH; t += 256) {
+            const int64_t r = c0 + t;
             int64_t sr = -1;
-            if (gr < r_end) {
-                sr = a.ids ? a.ids[gr] : gr;
+            if (r < r_end) {
+                sr = a.ids ? a.ids[r] : r;
                 if (sr < 0 || sr >= a.src_rows) sr = -1;
             }
-            srow[tid] = sr;
+            srow_s[t] = sr;
         }
         __syncthreads();
-        for (int e = tid; e < DW_R * DW_T; e += 256) {
-            const int rr = e / DW_T, cc = e % DW_T;
-            const int64_t gr = r0 + rr;
-            const int gn = n0 + cc, gk = k0 + cc;
-            float dz = 0.f, av = 0.f;
-            if (gr < r_end) {
-                if (gn < n) dz = a.dz_ws[gr * n + gn];
-                const int64_t sr = srow[rr];
-                if (gk < k && sr >= 0) av = pro_apply(pro, gr, gk, a.src[sr * a.ld_src + gk]);
-            }
-            DzT[cc * DW_LD + rr] = dz;
-            AT[cc * DW_LD + rr] = av;
-        }
-        __syncthreads();
-        const float* dp = DzT + (wn * 32 + c32) * DW_LD + h;
-        const float* ap = AT + (wk * 32 + c32) * DW_LD + h;
+        const int64_t c1 = (c0 + CH) < r_end ? (c0 + CH) : r_end;
+        for (int64_t r0 = c0; r0 < c1; r0 += 2 * U) {
+            float dv[U], raw[U];
 #pragma unroll
-        for (int s = 0; s < DW_R / 2; ++s) acc = mfma(dp[2 * s], ap[2 * s], acc);
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = r0 + 2 * u + h;
+                const int64_t sr = (r < c1) ? srow_s[r - c0] : -1;
+                dv[u] = (r < c1 && n_ok) ? a.dz_ws[r * n + gn] : 0.f;
+                raw[u] = (sr >= 0 && k_ok) ? a.src[sr * a.ld_src + gk] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = r0 + 2 * u + h;
+                const bool ok = r < c1 && k_ok && srow_s[(r < c1 ? r : c0) - c0] >= 0;
+                const float av = ok ? pro_apply(pro, r, gk, raw[u]) : 0.f;
+                acc = mfma(dv[u], av, acc);
+            }
+        }
     }
-    const int gk = k0 + wk * 32 + c32;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-        const int gn = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (gn < n && gk < k) atomicAdd(&a.dw[static_cast<int64_t>(gn) * k + gk], acc[r]);
+        const int on = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (on < n && k_ok) atomicAdd(&a.dw[static_cast<int64_t>(on) * k + gk], acc[r]);
     }
 }
 
@@ -439,26 +576,30 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
     if (!args) return RT_ERR_INVALID;
     const rt_linear_fwd_args& a = *args;
     if (a.m < 0 || a.k <= 0 || a.n <= 0 || !a.src || !a.w || a.ld_src < a.k) return RT_ERR_INVALID;
-    if (a.n > 512 || a.k > 4096) return RT_ERR_UNSUPPORTED;
+    if (a.n > 512 || a.k > 8192) return RT_ERR_UNSUPPORTED;
     if (a.prev_mode < 0 || a.prev_mode > 3) return RT_ERR_INVALID;
     if (a.prev_mode == 1 && (!a.prev_stats || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
-    if (a.l2_out && a.n > 512) return RT_ERR_UNSUPPORTED;
     if (a.m == 0) return RT_OK;
-    const int tpw = a.n <= 64 ? 1 : a.n <= 128 ? 2 : a.n <= 256 ? 4 : 8;
-    const int np = 64 * tpw;
-    const int kpad = (a.k + mlp::KC - 1) / mlp::KC * mlp::KC;
-    const size_t lds = (2 * kpad + mlp::BM * mlp::LDK + np * mlp::LDK + (np / 32) * mlp::BM) * sizeof(float) +
-                       mlp::BM * sizeof(int64_t) + 16;
+    const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
+    const int kp = mlp::pad8(a.k);
+    const size_t lds = (2 * kp + mlp::FM * (kp + 4) + 4 * tpw * mlp::FM) * sizeof(float) +
+                       mlp::FM * sizeof(int64_t) + 16;
     if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
-    const dim3 grid(static_cast<unsigned>((a.m + mlp::BM - 1) / mlp::BM));
+    const bool kvec = (a.k % 4) == 0 && (reinterpret_cast<uintptr_t>(a.w) & 15) == 0;
+    const dim3 grid(static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM));
     hipStream_t st = as_stream(stream);
-    switch (tpw) {
-        case 1: allow_lds(mlp::linear_fwd_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_fwd_kernel<1>, grid, dim3(256), lds, st, a); break;
-        case 2: allow_lds(mlp::linear_fwd_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_fwd_kernel<2>, grid, dim3(256), lds, st, a); break;
-        case 4: allow_lds(mlp::linear_fwd_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_fwd_kernel<4>, grid, dim3(256), lds, st, a); break;
-        default: allow_lds(mlp::linear_fwd_kernel<8>, lds); hipLaunchKernelGGL(mlp::linear_fwd_kernel<8>, grid, dim3(256), lds, st, a); break;
+#define RT_FWD(T, V)                                                                              \
+    do {                                                                                          \
+        allow_lds(mlp::linear_fwd_kernel<T, V>, lds);                                             \
+        hipLaunchKernelGGL((mlp::linear_fwd_kernel<T, V>), grid, dim3(256), lds, st, a);          \
+    } while (0)
+    if (kvec) {
+        if (tpw == 1) RT_FWD(1, true); else if (tpw == 2) RT_FWD(2, true); else RT_FWD(4, true);
+    } else {
+        if (tpw == 1) RT_FWD(1, false); else if (tpw == 2) RT_FWD(2, false); else RT_FWD(4, false);
     }
+#undef RT_FWD
     return check_launch("linear_fwd_kernel");
 }
 
@@ -468,7 +609,7 @@ extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
     if (a.m < 0 || a.k <= 0 || a.n <= 0 || !a.w || !a.dw || !a.dz_ws || !a.src || a.ld_src < a.k)
         return RT_ERR_INVALID;
     const bool need_da = a.g_prev || a.dsrc;
-    if (a.n > 256 || (need_da && a.k > 512)) return RT_ERR_UNSUPPORTED;
+    if (a.n > 2048 || (need_da && a.k > 512)) return RT_ERR_UNSUPPORTED;
     if (a.grad_mode == 0 && (!a.dout || !a.l2_out || !a.norms)) return RT_ERR_INVALID;
     if (a.grad_mode >= 1 && a.grad_mode <= 3 && (!a.g || !a.z)) return RT_ERR_INVALID;
     if ((a.grad_mode == 1 || a.grad_mode == 2) && (!a.g_stats || !a.save_mean || !a.save_invstd || !a.bn_gamma))
@@ -480,18 +621,14 @@ extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
     if (a.m == 0) return RT_OK;
     hipStream_t st = as_stream(stream);
     {
-        const int tpwk = !need_da ? 1 : a.k <= 64 ? 1 : a.k <= 128 ? 2 : a.k <= 256 ? 4 : 8;
-        const int kp = need_da ? 64 * tpwk : 0;
-        const int npad = (a.n + mlp::KC - 1) / mlp::KC * mlp::KC;
-        const size_t lds = (static_cast<size_t>(mlp::BM) * (npad + 1) + static_cast<size_t>(kp) * mlp::LDK) *
-                           sizeof(float);
-        if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
-        const dim3 grid(static_cast<unsigned>((a.m + mlp::BM - 1) / mlp::BM));
+        const int tpwk = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
+        const int np = mlp::pad8(a.n);
+        const size_t lds = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) + 16;
+        const dim3 grid(static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM));
         switch (tpwk) {
             case 1: allow_lds(mlp::linear_bwd_dz_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<1>, grid, dim3(256), lds, st, a); break;
             case 2: allow_lds(mlp::linear_bwd_dz_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<2>, grid, dim3(256), lds, st, a); break;
-            case 4: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, a); break;
-            default: allow_lds(mlp::linear_bwd_dz_kernel<8>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<8>, grid, dim3(256), lds, st, a); break;
+            default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, a); break;
         }
         const int rc = check_launch("linear_bwd_dz_kernel");
         if (rc) return rc;
@@ -504,7 +641,7 @@ extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
         if (splits > max_splits) splits = max_splits;
         if (splits < 1) splits = 1;
         int64_t rps = (a.m + splits - 1) / splits;
-        rps = (rps + mlp::DW_R - 1) / mlp::DW_R * mlp::DW_R;
+        rps = (rps + 15) / 16 * 16;
         splits = (a.m + rps - 1) / rps;
         const dim3 grid(static_cast<unsigned>(tn), static_cast<unsigned>(tk), static_cast<unsigned>(splits));
         hipLaunchKernelGGL(mlp::linear_bwd_dw_kernel, grid, dim3(256), 0, st, a, rps);

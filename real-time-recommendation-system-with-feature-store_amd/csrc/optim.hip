@@ -11,9 +11,14 @@ constexpr int kChunk = 4096;  // elements per block in the norm pass
 
 __global__ __launch_bounds__(256) void grad_sqnorm_kernel(const float* __restrict__ g,
                                                           const int64_t* __restrict__ offsets,
-                                                          double* __restrict__ out) {
+                                                          double* __restrict__ out, int32_t* step_counter,
+                                                          int64_t* seed_counter) {
     __shared__ double red[4];
     const int t = blockIdx.y;
+    if (blockIdx.x == 0 && t == 0 && threadIdx.x == 0) {
+        if (step_counter) *step_counter += 1;
+        if (seed_counter) *seed_counter += 1;
+    }
     const int64_t lo = offsets[t], hi = offsets[t + 1];
     if (lo + static_cast<int64_t>(blockIdx.x) * kChunk >= hi) return;  // uniform per block
     double s = 0.0;
@@ -73,13 +78,14 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, c
 using namespace rt;
 
 extern "C" int rt_grad_sqnorm(const float* grads, const int64_t* offsets, int n_tensors, double* sumsq_out,
-                              void* stream) {
+                              int32_t* step_counter, int64_t* seed_counter, void* stream) {
     if (n_tensors < 0 || (n_tensors > 0 && (!grads || !offsets || !sumsq_out))) return RT_ERR_INVALID;
     if (n_tensors == 0) return RT_OK;
     // offsets live on the device: 64 blocks per tensor, each striding over chunks;
     // blocks past a small tensor's end exit at once
     const dim3 grid(64, static_cast<unsigned>(n_tensors));
-    hipLaunchKernelGGL(optim::grad_sqnorm_kernel, grid, dim3(256), 0, as_stream(stream), grads, offsets, sumsq_out);
+    hipLaunchKernelGGL(optim::grad_sqnorm_kernel, grid, dim3(256), 0, as_stream(stream), grads, offsets, sumsq_out,
+                       step_counter, seed_counter);
     return check_launch("grad_sqnorm_kernel");
 }
 

@@ -67,9 +67,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 // keep element (row, col) of a dropout layer with probability 1-p
+// (32-bit murmur3 finaliser over seed/row/col: ~10 VALU ops per element)
 __device__ __forceinline__ bool dropout_keep(uint64_t seed, int64_t row, int col, float p) {
-    const uint64_t h = mix64(seed ^ mix64(static_cast<uint64_t>(row) * 0x100000001B3ull + static_cast<uint64_t>(col)));
-    const float u = static_cast<float>(h >> 40) * (1.0f / 16777216.0f);  // [0,1), 24 bits
+    uint32_t h = static_cast<uint32_t>(seed ^ (seed >> 32)) ^ (static_cast<uint32_t>(row) * 0x9E3779B1u) ^
+                 (static_cast<uint32_t>(col) * 0x85EBCA77u) ^ (static_cast<uint32_t>(row >> 32) * 0xC2B2AE3Du);
+    h ^= h >> 16;
+    h *= 0x85EBCA6Bu;
+    h ^= h >> 13;
+    h *= 0xC2B2AE35u;
+    h ^= h >> 16;
+    const float u = static_cast<float>(h >> 8) * (1.0f / 16777216.0f);  // [0,1), 24 bits
     return u >= p;
 }
 

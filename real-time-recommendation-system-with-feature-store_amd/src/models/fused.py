@@ -137,6 +137,7 @@ class ParamSlab:
             if old is not None:
                 p.grad.copy_(old)
         self.params, self.offsets, self.data, self.grad = ps, offs, data, grad
+        self.__dict__["_grad_views"] = {}
         ends = [o + s for o, s in zip(offs, sizes)]
         self.bounds = list(zip(offs, ends))
         self.offsets_dev = None
@@ -155,9 +156,15 @@ class ParamSlab:
                 p.grad = view.view(p.shape)
 
     def grad_of(self, p: torch.Tensor) -> torch.Tensor:
+        cache = self.__dict__.setdefault("_grad_views", {})
+        v = cache.get(id(p))
+        if v is not None and v[0] is p and v[1].data_ptr() >= self.grad.data_ptr():
+            return v[1]
         for q, (o, e) in zip(self.params, self.bounds):
             if q is p:
-                return self.grad[o:e].view(p.shape)
+                view = self.grad[o:e].view(p.shape)
+                cache[id(p)] = (p, view)
+                return view
         raise KeyError("parameter not in slab")
 
     def tensor_offsets(self) -> torch.Tensor:
@@ -192,8 +199,14 @@ def _stream(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+def stats_arena_size(blocks: List[Block]) -> int:
+    """fp64 words of BN column sums one forward (or backward) of the chain needs."""
+    return max(1, 2 * sum(b.linear.out_features for b in blocks[:-1]))
+
+
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
-                  normalize: bool = True, seed_offset: Optional[torch.Tensor] = None) -> ChainCtx:
+                  normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
+                  stats_arena: Optional[torch.Tensor] = None) -> ChainCtx:
     """Run the block chain. ``src`` is the dense input [rows, k0] (fp32) or a
     feature table when ``ids`` selects its rows (fused gather)."""
     native.require_device(src, what="tower forward")
@@ -216,7 +229,8 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
     ctx = ChainCtx(m=m, src=src, ids=ids, normalize=normalize)
     # one fp64 arena for all BN column sums of this call
     widths = [b.linear.out_features for b in blocks[:-1]]
-    stats_arena = torch.zeros(max(1, 2 * sum(widths)), dtype=torch.float64, device=dev)
+    if stats_arena is None:  # caller-provided arenas are zeroed by the caller (one memset per step)
+        stats_arena = torch.zeros(stats_arena_size(blocks), dtype=torch.float64, device=dev)
     stats, off = [], 0
     for wdt in widths:
         stats.append(stats_arena[off:off + 2 * wdt])
@@ -257,8 +271,8 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
                 a.save_invstd = si.data_ptr()
                 a.bn_eps = float(pb.bn.eps)
                 a.bn_momentum = float(pb.bn.momentum if pb.bn.momentum is not None else 0.1)
-                if pb.bn.training:
-                    pb.bn.num_batches_tracked.add_(1)
+                if pb.bn.training and pb.bn.num_batches_tracked is not None:
+                    a.num_batches_tracked = pb.bn.num_batches_tracked.data_ptr()  # +1 in-kernel
         a.act = b.act
         if li < L:
             z = torch.empty((m, lin.out_features), dtype=torch.float32, device=dev)
@@ -288,7 +302,8 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
 
 
 def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab: ParamSlab,
-                   want_dsrc: bool = False, seed_offset: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+                   want_dsrc: bool = False, seed_offset: Optional[torch.Tensor] = None,
+                   stats_arena: Optional[torch.Tensor] = None, attach: bool = True) -> Optional[torch.Tensor]:
     """Backward through the chain; parameter grads are atomically accumulated
     into the slab. Returns d src (dense input) when ``want_dsrc``."""
     dev = dout.device
@@ -296,11 +311,13 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
     m = ctx.m
     L = len(blocks) - 1
     st = _stream(dout)
-    slab.attach_grads()
+    if attach:
+        slab.attach_grads()
     max_w = max(b.linear.out_features for b in blocks)
     dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev)
     widths = [b.linear.out_features for b in blocks[:-1]]
-    gst_arena = torch.zeros(max(1, 2 * sum(widths)), dtype=torch.float64, device=dev)
+    gst_arena = stats_arena if stats_arena is not None else \
+        torch.zeros(stats_arena_size(blocks), dtype=torch.float64, device=dev)
     gstats, off = [], 0
     for wdt in widths:
         gstats.append(gst_arena[off:off + 2 * wdt])

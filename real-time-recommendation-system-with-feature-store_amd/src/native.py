@@ -49,6 +49,7 @@ class LinearFwdArgs(ctypes.Structure):
         ("running_mean", vp), ("running_var", vp), ("save_mean", vp), ("save_invstd", vp),
         ("bn_eps", c_f32), ("bn_momentum", c_f32), ("drop_p", c_f32), ("drop_seed", c_u64),
         ("seed_offset", vp), ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
+        ("num_batches_tracked", vp),
     ]
 
 
@@ -85,7 +86,7 @@ SIGNATURES = {
     "rt_twotower_loss_fwd": (c_int, [vp, vp, vp, c_int, c_i64, c_int, c_int, c_f32, vp, vp, c_f32, c_f32,
                                      vp, vp, c_size, vp]),
     "rt_similarity_f32": (c_int, [vp, vp, c_i64, c_int, c_f32, vp, vp, vp, vp]),
-    "rt_grad_sqnorm": (c_int, [vp, vp, c_int, vp, vp]),
+    "rt_grad_sqnorm": (c_int, [vp, vp, c_int, vp, vp, vp, vp]),
     "rt_clip_adam_step": (c_int, [vp, vp, vp, vp, c_i64, vp, c_int, c_f32, c_f32, vp, c_f32, c_f32, c_f32,
                                   c_f32, c_int, vp, vp]),
 }

@@ -19,7 +19,7 @@ from typing import Dict, Optional
 import torch
 
 from .. import kernels, native
-from ..models.fused import blocks_from_sequential, chain_backward, chain_forward
+from ..models.fused import blocks_from_sequential, chain_backward, chain_forward, stats_arena_size
 from ..models.two_tower import TwoTowerModel
 from ..native import call, ptr
 from ..profiling import TIMER
@@ -40,8 +40,17 @@ class FusedTrainStep:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr_dev = torch.tensor([lr], dtype=torch.float32, device=dev)
         self.seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # dropout mask counter
-        self.sumsq = torch.zeros(len(self.slab.params), dtype=torch.float64, device=dev)
-        self.loss_buf = torch.zeros(3, dtype=torch.float64, device=dev)
+        # ONE fp64 arena zeroed per step: BN sums of the 3 tower calls (fwd + bwd),
+        # the loss triple and the per-tensor grad norms
+        ua = stats_arena_size(blocks_from_sequential(model.user_tower.mlp))
+        ia = stats_arena_size(blocks_from_sequential(model.item_tower.mlp))
+        self._arena_sizes = [ua, ia, ia, ua, ia, ia, 3, len(self.slab.params)]
+        self.arena = torch.zeros(sum(self._arena_sizes), dtype=torch.float64, device=dev)
+        parts, off = [], 0
+        for sz in self._arena_sizes:
+            parts.append(self.arena[off:off + sz])
+            off += sz
+        (self.a_uf, self.a_pf, self.a_nf, self.a_ub, self.a_pb, self.a_nb, self.loss_buf, self.sumsq) = parts
         self.lr, self.wd, self.max_norm = lr, weight_decay, max_norm
         self.b1, self.b2 = betas
         self.eps = eps
@@ -61,19 +70,18 @@ class FusedTrainStep:
         ib = blocks_from_sequential(m.item_tower.mlp)
         slab = self.slab
         st = native.stream_of(slab.data)
-        self.step_dev.add_(1)
-        self.seed_dev.add_(1)
         slab.grad.zero_()
+        self.arena.zero_()
         so = self.seed_dev
-        u = chain_forward(ub, user_src, user_ids, seed_offset=so)
-        p = chain_forward(ib, pos_src, pos_ids, seed_offset=so)
-        q = chain_forward(ib, neg_src, neg_ids, seed_offset=so) if (neg_src is not None) else None
+        u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
+        p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf)
+        q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
+            if (neg_src is not None) else None
         b, d = u.out.shape
         n_neg = (q.m // b) if q is not None else 0
         du = torch.empty_like(u.out)
         dp = torch.empty_like(p.out)
         dq = torch.empty_like(q.out) if q is not None else None
-        self.loss_buf.zero_()
         ws = kernels.workspace(self.dev, native.lib().rt_twotower_loss_workspace_bytes(b, d), "loss")
         ubias, ibias = m.user_bias, m.item_bias
         with TIMER.region("loss_fwd_bwd", flops=6.0 * b * b * d + 6.0 * b * (n_neg + 1) * d,
@@ -84,18 +92,17 @@ class FusedTrainStep:
                  ptr(slab.grad_of(ubias)) if ubias is not None else None,
                  ptr(slab.grad_of(ibias)) if ibias is not None else None, ptr(ws), ws.numel(), st)
         if q is not None:
-            chain_backward(ib, q, dq, slab, seed_offset=so)
-        chain_backward(ib, p, dp, slab, seed_offset=so)
-        chain_backward(ub, u, du, slab, seed_offset=so)
+            chain_backward(ib, q, dq, slab, seed_offset=so, stats_arena=self.a_nb, attach=False)
+        chain_backward(ib, p, dp, slab, seed_offset=so, stats_arena=self.a_pb, attach=False)
+        chain_backward(ub, u, du, slab, seed_offset=so, stats_arena=self.a_ub, attach=False)
         if self.pg is not None:  # data parallel: average the flat grad slab (one RCCL all-reduce)
             import torch.distributed as dist
             dist.all_reduce(slab.grad, op=dist.ReduceOp.SUM, group=self.pg)
             slab.grad.mul_(1.0 / dist.get_world_size(self.pg))
-        self.sumsq.zero_()
         nb = slab.data.numel() * 4.0
         with TIMER.region("clip_adam", flops=0.0, bytes_=nb * 7):
             call("rt_grad_sqnorm", ptr(slab.grad), ptr(slab.tensor_offsets()), len(slab.params), ptr(self.sumsq),
-                 st)
+                 ptr(self.step_dev), ptr(self.seed_dev), st)
             call("rt_clip_adam_step", ptr(slab.data), ptr(slab.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
                  slab.data.numel(), ptr(self.sumsq), len(slab.params), self.max_norm, self.lr, ptr(self.lr_dev),
                  self.b1, self.b2, self.eps, self.wd, 1, ptr(self.step_dev), st)

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the fused tower-MLP kernels in isolation (GPU box).
+
+Times rt_linear_fwd_f32 / rt_linear_bwd_f32 for the C2 tower shapes with and
+without the BN/dropout prologue, to attribute the per-launch cost.
+Usage: python tools/microbench_mlp.py
+"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "real-time-recommendation-system-with-feature-store_amd")]
+
+import torch  # noqa: E402
+
+from src import native  # noqa: E402
+from src.native import LinearBwdArgs, LinearFwdArgs, call  # noqa: E402
+
+
+def timeit(fn, reps=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3  # us
+
+
+def main():
+    dev = torch.device("cuda:0")
+    native.lib()
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    print(f"{'case':44s} {'us':>8s} {'TF/s':>7s}")
+    for (m, k, n) in [(1024, 256, 128), (16384, 256, 128), (16384, 20, 256), (16384, 128, 128), (1024, 3, 256)]:
+        src = torch.randn(m, k, device=dev)
+        w = torch.randn(n, k, device=dev) * 0.05
+        b = torch.zeros(n, device=dev)
+        z = torch.empty(m, n, device=dev)
+        stats_prev = torch.zeros(2 * k, dtype=torch.float64, device=dev)
+        stats_prev[:k] = 0.1 * m
+        stats_prev[k:] = 1.0 * m
+        gam = torch.ones(k, device=dev)
+        bet = torch.zeros(k, device=dev)
+        rm = torch.zeros(k, device=dev)
+        rv = torch.ones(k, device=dev)
+        sm = torch.empty(k, device=dev)
+        si = torch.empty(k, device=dev)
+        stats = torch.zeros(2 * n, dtype=torch.float64, device=dev)
+        for label, mode, drop, want_stats in [("raw", 0, 0.0, False), ("raw+stats", 0, 0.0, True),
+                                              ("bn-train", 1, 0.0, True), ("bn-train+drop", 1, 0.2, True)]:
+            a = LinearFwdArgs()
+            a.src, a.src_rows, a.ld_src, a.m, a.k, a.n = src.data_ptr(), m, k, m, k, n
+            a.w, a.bias, a.z_out, a.act = w.data_ptr(), b.data_ptr(), z.data_ptr(), 0
+            a.prev_mode, a.prev_act = mode, 0
+            if mode == 1:
+                a.prev_stats, a.bn_gamma, a.bn_beta = stats_prev.data_ptr(), gam.data_ptr(), bet.data_ptr()
+                a.running_mean, a.running_var = rm.data_ptr(), rv.data_ptr()
+                a.save_mean, a.save_invstd = sm.data_ptr(), si.data_ptr()
+                a.bn_eps, a.bn_momentum = 1e-5, 0.1
+            a.drop_p, a.drop_seed = drop, 7
+            if want_stats:
+                a.stats_out = stats.data_ptr()
+            us = timeit(lambda: call("rt_linear_fwd_f32", ctypes.byref(a), st))
+            print(f"fwd m={m:5d} k={k:3d} n={n:3d} {label:14s} {us:8.1f} {2 * m * k * n / us / 1e6:7.2f}")
+        # backward (hidden-layer form: BN-train grad, dA with stats)
+        g = torch.randn(m, n, device=dev)
+        dz = torch.empty(m, n, device=dev)
+        dw = torch.zeros(n, k, device=dev)
+        db = torch.zeros(n, device=dev)
+        gst = torch.zeros(2 * n, dtype=torch.float64, device=dev)
+        gprev = torch.empty(m, k, device=dev)
+        gprev_st = torch.zeros(2 * k, dtype=torch.float64, device=dev)
+        smn = torch.zeros(n, device=dev)
+        sin = torch.ones(n, device=dev)
+        gn = torch.ones(n, device=dev)
+        dgn = torch.zeros(n, device=dev)
+        dbn = torch.zeros(n, device=dev)
+        for label, want_da in [("dz+dW", False), ("dz+dA+dW", True)]:
+            a = LinearBwdArgs()
+            a.m, a.k, a.n, a.w, a.dw, a.dbias, a.dz_ws = m, k, n, w.data_ptr(), dw.data_ptr(), db.data_ptr(), dz.data_ptr()
+            a.grad_mode, a.g, a.z, a.act = 1, g.data_ptr(), z.data_ptr(), 0
+            a.g_stats, a.save_mean, a.save_invstd, a.bn_gamma = gst.data_ptr(), smn.data_ptr(), sin.data_ptr(), gn.data_ptr()
+            a.dgamma, a.dbeta = dgn.data_ptr(), dbn.data_ptr()
+            a.src, a.src_rows, a.ld_src = src.data_ptr(), m, k
+            a.prev_mode, a.prev_act = 1, 0
+            a.prev_mean, a.prev_invstd, a.prev_gamma, a.prev_beta = sm.data_ptr(), si.data_ptr(), gam.data_ptr(), bet.data_ptr()
+            if want_da:
+                a.g_prev, a.g_prev_stats = gprev.data_ptr(), gprev_st.data_ptr()
+            us = timeit(lambda: call("rt_linear_bwd_f32", ctypes.byref(a), st))
+            fl = (4 if want_da else 2) * m * k * n
+            print(f"bwd m={m:5d} k={k:3d} n={n:3d} {label:14s} {us:8.1f} {fl / us / 1e6:7.2f}")
+
+
+if __name__ == "__main__":
+    main()
