@@ -114,9 +114,16 @@ int rt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int n_lis
  *             3: a = drop(act_prev(A))   (no BN: ItemTower.content_projection)
  *   drop: keep with prob 1-p, scale 1/(1-p), mask = hash(drop_seed, r, col)
  *   z = a · Wᵀ + bias   (W [n, k] row-major, n <= 512)  → z_out [m, n]
- *   stats_out (caller-zeroed fp64 [2n]) += (Σ_r act(z), Σ_r act(z)^2)
+ *   stats_out (caller-zeroed) += (Σ_r act(z), Σ_r act(z)^2)
  *   l2_out: F.normalize(z, p=2, eps=1e-12) rows, norms_out[r] = ||z[r]||
+ *
+ * BatchNorm column sums (stats_out / prev_stats / g_stats / g_prev_stats) are
+ * fp64 [RT_STAT_SLOTS][2][width]: row block b adds its partial sums into slot
+ * b % RT_STAT_SLOTS (bounds same-address atomic contention), consumers sum the
+ * slots in slot order. Caller zeroes them before the producing launch.
  * ------------------------------------------------------------------------ */
+#define RT_STAT_SLOTS 16
+
 typedef struct {
     const float* src;        /* [src_rows, ld_src] input rows (features or prev z) */
     int64_t src_rows;        /* rows in src (bounds for gather)                       */
@@ -129,7 +136,7 @@ typedef struct {
     const float* bias;       /* [n] or NULL                                            */
     int prev_mode;           /* 0 raw, 1 BN train, 2 BN eval, 3 act+dropout only        */
     int prev_act;            /* rt_act of the previous block                           */
-    const double* prev_stats;/* [2k] fp64 sums (mode 1)                                */
+    const double* prev_stats;/* [RT_STAT_SLOTS][2k] fp64 sums (mode 1)                 */
     const float* bn_gamma;   /* [k]                                                    */
     const float* bn_beta;    /* [k]                                                    */
     float* running_mean;     /* [k] read (mode 2) / updated (mode 1, may be NULL)      */
@@ -143,7 +150,7 @@ typedef struct {
     const uint64_t* seed_offset; /* device counter (hipGraph replay draws new masks)   */
     float* z_out;            /* [m, n] pre-activation, or NULL                         */
     int act;                 /* activation of THIS block (for stats_out)               */
-    double* stats_out;       /* [2n] accumulated (NULL = skip)                         */
+    double* stats_out;       /* [RT_STAT_SLOTS][2n] accumulated (NULL = skip)          */
     float* l2_out;           /* [m, n] normalized rows (final layer) or NULL          */
     float* norms_out;        /* [m] row norms (with l2_out)                            */
     int64_t* num_batches_tracked; /* prev BN counter, +1 by block 0 in mode 1 (may be NULL) */
@@ -158,9 +165,11 @@ int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
  *             3: dz = act'(z)·g                                   (no BN)
  *      with g = d loss/d(BN output) [m, n], x̂ = (act(z) − save_mean)·save_invstd.
  *   dz_ws [m, n] receives dz; dbias += Σ_r dz; dw += dzᵀ·a  (fp32 atomics into
- *   caller-zeroed buffers), a = the forward input of this Linear recomputed by
- *   the same prologue (src/ids/prev_* exactly as passed to rt_linear_fwd_f32).
- *   modes 1/2: dgamma += Σ g·x̂, dbeta += Σ g (read from g_stats).
+ *   caller-zeroed buffers, one per output element per M-split of at most 32),
+ *   a = the forward input of this Linear recomputed by the same prologue
+ *   (src/ids/prev_* exactly as passed to rt_linear_fwd_f32).
+ *   modes 1/2: dgamma += Σ g·x̂, dbeta += Σ g (read from g_stats; atomic, so two
+ *   chains of one tower may run concurrently on different streams).
  *   da = dz·W [m, k] then: dsrc = da (if non-NULL; input gradient, layer 1) and/or
  *   g_prev = drop_bwd_prev(da) with g_prev_stats += (Σ g_prev, Σ g_prev·x̂_prev)
  *   (x̂_prev from src with prev_mean/prev_invstd; prev_mode 1/2 only).
@@ -178,7 +187,7 @@ typedef struct {
     const float* g;          /* modes 1-3: [m, n] */
     const float* z;          /* modes 1-3: [m, n] pre-activation of this block */
     int act;                 /* this block's activation */
-    const double* g_stats;   /* modes 1,2: [2n] (Σg, Σg·x̂) */
+    const double* g_stats;   /* modes 1,2: [RT_STAT_SLOTS][2n] (Σg, Σg·x̂) */
     const float* save_mean;  /* [n] */
     const float* save_invstd;/* [n] */
     const float* bn_gamma;   /* [n] */
@@ -192,7 +201,7 @@ typedef struct {
     float prev_drop_p; uint64_t prev_drop_seed; const uint64_t* seed_offset;
     /* outputs towards the previous block */
     float* g_prev;           /* [m, k] or NULL */
-    double* g_prev_stats;    /* [2k] accumulated, caller zeroes (NULL = skip) */
+    double* g_prev_stats;    /* [RT_STAT_SLOTS][2k] accumulated, caller zeroes (NULL = skip) */
     float* dsrc;             /* [m, k] input grad (first layer), or NULL */
 } rt_linear_bwd_args;
 

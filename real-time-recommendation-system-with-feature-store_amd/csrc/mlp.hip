@@ -11,8 +11,9 @@
 //   epilogue  : bias, pre-activation store, fp64 column stats of act(z) for the
 //               next BatchNorm, or (final layer) the row L2 normalisation.
 // Backward is two launches per Linear: (1) dz (normalize/BN/act backward) +
-// dbias + dA = dz·W with the previous block's dropout/BN-stat epilogue,
-// (2) dW = dzᵀ·A over M split across blocks, A recomputed by the same prologue.
+// dgamma/dbeta + dA = dz·W with the previous block's dropout/BN-stat epilogue,
+// (2) dW = dzᵀ·A and dbias over M split across blocks, A recomputed by the
+// same prologue. BN column sums go to RT_STAT_SLOTS fp64 slots (include/rtrec_hip.h).
 #include "rt_common.h"
 
 namespace rt {
@@ -85,8 +86,14 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
         for (int c = tid; c < k; c += 256) {
             float mean, invstd, var_f = 0.f;
             if (a.prev_mode == 1) {
-                const double md = a.prev_stats[c] / static_cast<double>(m);
-                double vd = a.prev_stats[k + c] / static_cast<double>(m) - md * md;
+                double s1 = 0.0, s2 = 0.0;  // slot sums in slot order
+#pragma unroll 4
+                for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                    s1 += a.prev_stats[static_cast<int64_t>(sl) * 2 * k + c];
+                    s2 += a.prev_stats[static_cast<int64_t>(sl) * 2 * k + k + c];
+                }
+                const double md = s1 / static_cast<double>(m);
+                double vd = s2 / static_cast<double>(m) - md * md;
                 vd = vd > 0.0 ? vd : 0.0;
                 mean = static_cast<float>(md);
                 invstd = static_cast<float>(1.0 / sqrt(vd + static_cast<double>(a.bn_eps)));
@@ -218,6 +225,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
 
     // ---- epilogue ----
     const bool l2 = a.l2_out != nullptr;
+    double* const stats = a.stats_out ? a.stats_out + static_cast<int64_t>(blockIdx.x % RT_STAT_SLOTS) * 2 * n : nullptr;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
         const int ct = w + 4 * i;
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
             acc[i][r] = z;
             const bool ok = col_ok && gr < m;
             if (ok && a.z_out) a.z_out[gr * n + col] = z;
-            if (ok && a.stats_out) {
+            if (ok && stats) {
                 const float av = act_fwd(a.act, z);
                 s1 += av;
                 s2 += av * av;
@@ -245,12 +253,12 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
                 if (c32 == 0) rowpart[ct * FM + lr] = q;
             }
         }
-        if (a.stats_out) {
+        if (stats) {
             s1 += __shfl_xor(s1, 32, 64);
             s2 += __shfl_xor(s2, 32, 64);
             if (h == 0 && col_ok) {
-                atomicAdd(&a.stats_out[col], static_cast<double>(s1));
-                atomicAdd(&a.stats_out[n + col], static_cast<double>(s2));
+                atomicAdd(&stats[col], static_cast<double>(s1));
+                atomicAdd(&stats[n + col], static_cast<double>(s2));
             }
         }
     }
@@ -277,7 +285,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
 }
 
 // ---------------------------------------------------------------------------
-// backward 1: dz, dbias, dgamma/dbeta, dA = dz·W (+ g_prev / dsrc epilogue)
+// backward 1: dz, dgamma/dbeta, dA = dz·W (+ g_prev / dsrc epilogue)
 // ---------------------------------------------------------------------------
 // Block = 32 rows. dz (32 x n) lives in LDS; dA = dz·W reads W[n][k] rows
 // coalesced along k straight from L2 (the reduction runs over n).
@@ -330,8 +338,14 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
                 M = a.save_mean[c];
                 A = a.bn_gamma[c] * I;
                 if (a.grad_mode == 1) {
-                    Bc = static_cast<float>(a.g_stats[c]) * inv_m;
-                    C = static_cast<float>(a.g_stats[n + c]) * inv_m;
+                    double gs1 = 0.0, gs2 = 0.0;
+#pragma unroll 4
+                    for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                        gs1 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + c];
+                        gs2 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + n + c];
+                    }
+                    Bc = static_cast<float>(gs1) * inv_m;
+                    C = static_cast<float>(gs2) * inv_m;
                 }
             }
             cA[c] = A; cB[c] = Bc; cC[c] = C; cM[c] = M; cI[c] = I;
@@ -394,19 +408,19 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
             }
         }
     }
-    __syncthreads();
-    for (int c = tid; c < n; c += 256) {
-        if (a.dbias) {
-            float s = 0.f;
-            for (int r = 0; r < FM; ++r) s += Dz[r * ldz + c];
-            atomicAdd(&a.dbias[c], s);
-        }
-        if (blockIdx.x == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
-            a.dgamma[c] += static_cast<float>(a.g_stats[n + c]);
-            a.dbeta[c] += static_cast<float>(a.g_stats[c]);
+    if (blockIdx.x == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
+        for (int c = tid; c < n; c += 256) {
+            double gs1 = 0.0, gs2 = 0.0;
+            for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                gs1 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + c];
+                gs2 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + n + c];
+            }
+            atomicAdd(&a.dgamma[c], static_cast<float>(gs2));  // atomic: concurrent chains of one tower
+            atomicAdd(&a.dbeta[c], static_cast<float>(gs1));
         }
     }
     if (!a.g_prev && !a.dsrc) return;
+    __syncthreads();
 
     // ---- phase B: dA = dz · W  (reduction over n, permuted per lane half) ----
     f32x16 acc[TPWK];
@@ -444,6 +458,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
     const float pscale = a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f;
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
+    double* const gps = want_stats ? a.g_prev_stats + static_cast<int64_t>(blockIdx.x % RT_STAT_SLOTS) * 2 * k : nullptr;
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
         const int kk = (w + 4 * i) * 32 + c32;
@@ -474,85 +489,172 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
             s1 += __shfl_xor(s1, 32, 64);
             s2 += __shfl_xor(s2, 32, 64);
             if (h == 0 && col_ok) {
-                atomicAdd(&a.g_prev_stats[kk], static_cast<double>(s1));
-                atomicAdd(&a.g_prev_stats[k + kk], static_cast<double>(s2));
+                atomicAdd(&gps[kk], static_cast<double>(s1));
+                atomicAdd(&gps[k + kk], static_cast<double>(s2));
             }
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// backward 2: dW[n][k] += Σ_r dz[r][n] · A[r][k], M split over blockIdx.z
+// backward 2: dW[n][k] += Σ_r dz[r][n] · A[r][k] (+ dbias[n] += Σ_r dz[r][n]),
+// M split over blockIdx.z
 // ---------------------------------------------------------------------------
-constexpr int DW_T = 64;   // output tile (n) x (k); 4 waves of 32x32
+// Every wave owns a 64(n) x 32·KT(k) tile (2·KT independent 32x32 accumulators)
+// over its own contiguous slice of the block's rows, so the main loop has no
+// barrier: each k-step (2 rows) a lane loads dz[r][n0+c32], dz[r][n0+32+c32]
+// and A[r][k0+32j+c32] straight from L2/HBM (128 B per half-wave), groups of
+// U k-steps are double-buffered in registers (the next group's loads fly
+// during the current group's MFMAs), and the A prologue (act → BN affine →
+// dropout) runs on registers with per-lane column constants. The 4 waves'
+// tiles are summed through LDS and added to dW with one fp32 atomic per
+// element per block (<= 32 splits, see the host).
+//   PRO: 0 raw A, 1 piecewise-linear act, 2 same + dropout, 3 generic act.
+constexpr int DW_N = 64;      // n per block/wave
+constexpr int DW_SEG = 2048;  // rows whose gather ids are staged in LDS at a time
+constexpr int DW_U = 4;       // k-steps (2 rows each) per register group
 
-// No LDS: lane c of a wave reads dz[r][n0+c] and A[r][k0+c] for the rows of
-// its MFMA k-step (32 consecutive floats per half-wave = one coalesced line),
-// A recomputed by the forward prologue; 8 k-steps unrolled so 16 independent
-// loads are in flight per wave.
+template <int PRO>
+__device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, int c, float sc, float sh, float v) {
+    if constexpr (PRO == 0) {
+        return v;
+    } else {
+        if constexpr (PRO == 3) v = act_fwd(p.act, v);
+        else v = act_pwl(slope, v);
+        v = __builtin_fmaf(v, sc, sh);
+        if constexpr (PRO == 2) v = dropout_keep(p.seed, r, c, p.drop_p) ? v * p.drop_scale : 0.f;
+        if constexpr (PRO == 3) {
+            if (p.drop_p > 0.f) v = dropout_keep(p.seed, r, c, p.drop_p) ? v * p.drop_scale : 0.f;
+        }
+        return v;
+    }
+}
+
+template <int KT, int PRO>
 __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a, int64_t rows_per_split) {
-    __shared__ float scale[DW_T], shift[DW_T];
+    constexpr int NT = 2, U = DW_U;
+    constexpr int NV = NT * KT * 16;  // accumulator registers per lane
+    __shared__ int srow[DW_SEG];
+    __shared__ float red[4][NV][64];
+    __shared__ float bred[4][DW_N];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
+    const int n0 = blockIdx.x * DW_N, k0 = blockIdx.y * (32 * KT);
     const int64_t r_begin = static_cast<int64_t>(blockIdx.z) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
-    if (a.prev_mode == 1 || a.prev_mode == 2) {
-        for (int c = tid; c < DW_T; c += 256) {
-            const int gc = k0 + c;
-            if (gc < k) bn_affine(a.prev_gamma[gc], a.prev_beta[gc], a.prev_mean[gc], a.prev_invstd[gc], scale[c], shift[c]);
-            else { scale[c] = 0.f; shift[c] = 0.f; }
+
+    int gn[NT], gk[KT];
+    bool n_ok[NT], k_ok[KT];
+    float sc[KT], sh[KT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) { gn[i] = n0 + 32 * i + c32; n_ok[i] = gn[i] < n; }
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        gk[j] = k0 + 32 * j + c32;
+        k_ok[j] = gk[j] < k;
+        sc[j] = 1.f; sh[j] = 0.f;
+        if ((a.prev_mode == 1 || a.prev_mode == 2) && k_ok[j])
+            bn_affine(a.prev_gamma[gk[j]], a.prev_beta[gk[j]], a.prev_mean[gk[j]], a.prev_invstd[gk[j]], sc[j], sh[j]);
+    }
+    const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
+    const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
+                  pseed, nullptr, nullptr};
+    const float slope = act_slope(a.prev_act);
+    const bool do_bias = a.dbias != nullptr && blockIdx.y == 0;
+    const bool gather = a.ids != nullptr;
+
+    f32x16 acc[NT][KT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < KT; ++j) acc[i][j] = f32x16{};
+    float bsum[NT] = {};
+
+    float dA[U][NT], xA[U][KT], dB[U][NT], xB[U][KT];
+    int64_t seg0 = 0;
+    auto load = [&](float (&d)[U][NT], float (&x)[U][KT], int64_t g, int64_t we) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = g + 2 * u + h;
+            const bool rv = r < we;
+            int64_t sr = r;
+            if (gather) sr = rv ? srow[r - seg0] : -1;
+#pragma unroll
+            for (int i = 0; i < NT; ++i) d[u][i] = (rv && n_ok[i]) ? a.dz_ws[r * n + gn[i]] : 0.f;
+#pragma unroll
+            for (int j = 0; j < KT; ++j) x[u][j] = (rv && sr >= 0 && k_ok[j]) ? a.src[sr * a.ld_src + gk[j]] : 0.f;
+        }
+    };
+    auto compute = [&](float (&d)[U][NT], float (&x)[U][KT], int64_t g) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t r = g + 2 * u + h;
+#pragma unroll
+            for (int j = 0; j < KT; ++j) {
+                const float xa = pro_col<PRO>(pro, slope, r, gk[j], sc[j], sh[j], x[u][j]);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) acc[i][j] = mfma(d[u][i], xa, acc[i][j]);
+            }
+            if (do_bias) {
+#pragma unroll
+                for (int i = 0; i < NT; ++i) bsum[i] += d[u][i];
+            }
+        }
+    };
+
+    for (seg0 = r_begin; seg0 < r_end; seg0 += DW_SEG) {
+        const int64_t seg1 = (seg0 + DW_SEG) < r_end ? (seg0 + DW_SEG) : r_end;
+        if (gather) {
+            __syncthreads();
+            for (int t = tid; t < seg1 - seg0; t += 256) {
+                const int64_t id = a.ids[seg0 + t];
+                srow[t] = (id < 0 || id >= a.src_rows) ? -1 : static_cast<int>(id);
+            }
+            __syncthreads();
+        }
+        // this wave's contiguous slice of the segment (multiple of 2U rows)
+        const int64_t len = seg1 - seg0;
+        const int64_t per = ((len + 3) / 4 + 2 * U - 1) / (2 * U) * (2 * U);
+        const int64_t wb = seg0 + w * per;
+        const int64_t we = (wb + per) < seg1 ? (wb + per) : seg1;
+        if (wb >= we) continue;
+        load(dA, xA, wb, we);
+        for (int64_t g = wb; g < we; g += 4 * U) {
+            if (g + 2 * U < we) load(dB, xB, g + 2 * U, we);
+            compute(dA, xA, g);
+            if (g + 2 * U >= we) break;
+            if (g + 4 * U < we) load(dA, xA, g + 4 * U, we);
+            compute(dB, xB, g + 2 * U);
+        }
+    }
+
+    // ---- sum the 4 waves' tiles through LDS, one atomic per element ----
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < KT; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[w][(i * KT + j) * 16 + r][lane] = acc[i][j][r];
+    if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const float t = bsum[i] + __shfl_xor(bsum[i], 32, 64);
+            if (h == 0) bred[w][32 * i + c32] = t;
         }
     }
     __syncthreads();
-    const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
-    // scale/shift are indexed by the global column inside pro_apply: offset the base
-    const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
-                  pseed, scale - k0, shift - k0};
-    const int wn = w & 1, wk = w >> 1;
-    const int gn = n0 + wn * 32 + c32;   // this lane's dz column (A operand row)
-    const int gk = k0 + wk * 32 + c32;   // this lane's A column (B operand column)
-    const bool n_ok = gn < n, k_ok = gk < k;
-    f32x16 acc = f32x16{};
-    constexpr int U = 8;                 // k-steps per unrolled group (16 rows)
-    constexpr int CH = 256;              // rows whose source index is staged at a time
-    __shared__ int64_t srow_s[CH];
-    for (int64_t c0 = r_begin; c0 < r_end; c0 += CH) {
-        __syncthreads();
-        for (int t = tid; t < CH; t += 256) {
-            const int64_t r = c0 + t;
-            int64_t sr = -1;
-            if (r < r_end) {
-                sr = a.ids ? a.ids[r] : r;
-                if (sr < 0 || sr >= a.src_rows) sr = -1;
-            }
-            srow_s[t] = sr;
-        }
-        __syncthreads();
-        const int64_t c1 = (c0 + CH) < r_end ? (c0 + CH) : r_end;
-        for (int64_t r0 = c0; r0 < c1; r0 += 2 * U) {
-            float dv[U], raw[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t r = r0 + 2 * u + h;
-                const int64_t sr = (r < c1) ? srow_s[r - c0] : -1;
-                dv[u] = (r < c1 && n_ok) ? a.dz_ws[r * n + gn] : 0.f;
-                raw[u] = (sr >= 0 && k_ok) ? a.src[sr * a.ld_src + gk] : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t r = r0 + 2 * u + h;
-                const bool ok = r < c1 && k_ok && srow_s[(r < c1 ? r : c0) - c0] >= 0;
-                const float av = ok ? pro_apply(pro, r, gk, raw[u]) : 0.f;
-                acc = mfma(dv[u], av, acc);
-            }
-        }
+    for (int p = tid; p < NV * 64; p += 256) {
+        const int v = p >> 6, l = p & 63;
+        const float t = red[0][v][l] + red[1][v][l] + red[2][v][l] + red[3][v][l];
+        const int i = v / (KT * 16), j = (v / 16) % KT, rr = v & 15;
+        const int on = n0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * (l >> 5);
+        const int ok = k0 + 32 * j + (l & 31);
+        if (on < n && ok < k) atomicAdd(&a.dw[static_cast<int64_t>(on) * k + ok], t);
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int on = n0 + wn * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (on < n && k_ok) atomicAdd(&a.dw[static_cast<int64_t>(on) * k + gk], acc[r]);
+    if (do_bias && tid < DW_N) {
+        const int col = n0 + tid;
+        if (col < n) atomicAdd(&a.dbias[col], bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid]);
     }
 }
 
@@ -634,17 +736,29 @@ extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
         if (rc) return rc;
     }
     {
-        const int tn = (a.n + mlp::DW_T - 1) / mlp::DW_T;
-        const int tk = (a.k + mlp::DW_T - 1) / mlp::DW_T;
+        const int kt = a.k <= 32 ? 1 : 2;
+        const int tn = (a.n + mlp::DW_N - 1) / mlp::DW_N;
+        const int tk = (a.k + 32 * kt - 1) / (32 * kt);
+        // ~512 blocks (2 per CU), >= 64 rows per block, <= 32 splits per tile
         int64_t splits = (512 + tn * tk - 1) / (tn * tk);
         const int64_t max_splits = (a.m + 63) / 64;
         if (splits > max_splits) splits = max_splits;
+        if (splits > 32) splits = 32;
         if (splits < 1) splits = 1;
         int64_t rps = (a.m + splits - 1) / splits;
-        rps = (rps + 15) / 16 * 16;
+        rps = (rps + 63) / 64 * 64;
         splits = (a.m + rps - 1) / rps;
         const dim3 grid(static_cast<unsigned>(tn), static_cast<unsigned>(tk), static_cast<unsigned>(splits));
-        hipLaunchKernelGGL(mlp::linear_bwd_dw_kernel, grid, dim3(256), 0, st, a, rps);
+        int pro = 0;
+        if (a.prev_mode != 0)
+            pro = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
+#define RT_DW(KT, P) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<KT, P>), grid, dim3(256), 0, st, a, rps)
+        if (kt == 1) {
+            switch (pro) { case 0: RT_DW(1, 0); break; case 1: RT_DW(1, 1); break; case 2: RT_DW(1, 2); break; default: RT_DW(1, 3); }
+        } else {
+            switch (pro) { case 0: RT_DW(2, 0); break; case 1: RT_DW(2, 1); break; case 2: RT_DW(2, 2); break; default: RT_DW(2, 3); }
+        }
+#undef RT_DW
         return check_launch("linear_bwd_dw_kernel");
     }
 }

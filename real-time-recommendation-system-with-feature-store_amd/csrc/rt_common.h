@@ -91,6 +91,16 @@ __device__ __forceinline__ float act_fwd(int act, float z) {
         default: return z;
     }
 }
+// ReLU / LeakyReLU(0.1) / identity as ONE select (no per-element branch):
+// z > 0 ? z : slope * z
+__host__ __device__ __forceinline__ bool act_is_piecewise_linear(int act) {
+    return act == RT_ACT_RELU || act == RT_ACT_LEAKY_RELU || act == RT_ACT_NONE;
+}
+__host__ __device__ __forceinline__ float act_slope(int act) {
+    return act == RT_ACT_RELU ? 0.f : act == RT_ACT_LEAKY_RELU ? 0.1f : 1.f;
+}
+__device__ __forceinline__ float act_pwl(float slope, float z) { return z > 0.f ? z : slope * z; }
+
 // d act / dz evaluated at z
 __device__ __forceinline__ float act_bwd(int act, float z) {
     switch (act) {

@@ -199,9 +199,12 @@ def _stream(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
+STAT_SLOTS = 16  # RT_STAT_SLOTS (include/rtrec_hip.h): BN sums are [slots][2][width] fp64
+
+
 def stats_arena_size(blocks: List[Block]) -> int:
     """fp64 words of BN column sums one forward (or backward) of the chain needs."""
-    return max(1, 2 * sum(b.linear.out_features for b in blocks[:-1]))
+    return max(1, STAT_SLOTS * 2 * sum(b.linear.out_features for b in blocks[:-1]))
 
 
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
@@ -233,8 +236,8 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         stats_arena = torch.zeros(stats_arena_size(blocks), dtype=torch.float64, device=dev)
     stats, off = [], 0
     for wdt in widths:
-        stats.append(stats_arena[off:off + 2 * wdt])
-        off += 2 * wdt
+        stats.append(stats_arena[off:off + STAT_SLOTS * 2 * wdt])
+        off += STAT_SLOTS * 2 * wdt
     st = _stream(src)
     cur_src, cur_ids, ld = src, ids, src.shape[1]
     for li, b in enumerate(blocks):
@@ -320,8 +323,8 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         torch.zeros(stats_arena_size(blocks), dtype=torch.float64, device=dev)
     gstats, off = [], 0
     for wdt in widths:
-        gstats.append(gst_arena[off:off + 2 * wdt])
-        off += 2 * wdt
+        gstats.append(gst_arena[off:off + STAT_SLOTS * 2 * wdt])
+        off += STAT_SLOTS * 2 * wdt
     gs: List[Optional[torch.Tensor]] = [None] * L
     dsrc = torch.empty((m, blocks[0].linear.in_features), dtype=torch.float32, device=dev) if want_dsrc else None
     for li in range(L, -1, -1):

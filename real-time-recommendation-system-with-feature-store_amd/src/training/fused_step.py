@@ -58,6 +58,11 @@ class FusedTrainStep:
         self.steps = 0
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.static: Dict[str, torch.Tensor] = {}
+        # the user chain and the positive-item chain overlap the negative-item chain
+        # (three independent towers calls; BN running stats of the item tower still
+        # update pos → neg in order, as the reference's sequential calls do)
+        self.concurrent = True
+        self.side = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
 
     def set_lr(self, lr: float):
         self.lr = lr
@@ -73,10 +78,15 @@ class FusedTrainStep:
         slab.grad.zero_()
         self.arena.zero_()
         so = self.seed_dev
-        u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
+        main = torch.cuda.current_stream(self.dev)
+        s_u, s_p = self.side if self.concurrent else (main, main)
+        s_u.wait_stream(main)
+        with torch.cuda.stream(s_u):
+            u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
         p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf)
         q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
             if (neg_src is not None) else None
+        main.wait_stream(s_u)
         b, d = u.out.shape
         n_neg = (q.m // b) if q is not None else 0
         du = torch.empty_like(u.out)
@@ -91,10 +101,17 @@ class FusedTrainStep:
                  ptr(du), ptr(dp), ptr(dq),
                  ptr(slab.grad_of(ubias)) if ubias is not None else None,
                  ptr(slab.grad_of(ibias)) if ibias is not None else None, ptr(ws), ws.numel(), st)
+        # backward: three independent chains (grads meet in the slab through atomics)
+        s_u.wait_stream(main)
+        s_p.wait_stream(main)
+        with torch.cuda.stream(s_u):
+            chain_backward(ub, u, du, slab, seed_offset=so, stats_arena=self.a_ub, attach=False)
+        with torch.cuda.stream(s_p):
+            chain_backward(ib, p, dp, slab, seed_offset=so, stats_arena=self.a_pb, attach=False)
         if q is not None:
             chain_backward(ib, q, dq, slab, seed_offset=so, stats_arena=self.a_nb, attach=False)
-        chain_backward(ib, p, dp, slab, seed_offset=so, stats_arena=self.a_pb, attach=False)
-        chain_backward(ub, u, du, slab, seed_offset=so, stats_arena=self.a_ub, attach=False)
+        main.wait_stream(s_u)
+        main.wait_stream(s_p)
         if self.pg is not None:  # data parallel: average the flat grad slab (one RCCL all-reduce)
             import torch.distributed as dist
             dist.all_reduce(slab.grad, op=dist.ReduceOp.SUM, group=self.pg)

@@ -41,16 +41,17 @@ def main():
         w = torch.randn(n, k, device=dev) * 0.05
         b = torch.zeros(n, device=dev)
         z = torch.empty(m, n, device=dev)
-        stats_prev = torch.zeros(2 * k, dtype=torch.float64, device=dev)
+        S = 16  # RT_STAT_SLOTS
+        stats_prev = torch.zeros(S * 2 * k, dtype=torch.float64, device=dev)
         stats_prev[:k] = 0.1 * m
-        stats_prev[k:] = 1.0 * m
+        stats_prev[k:2 * k] = 1.0 * m
         gam = torch.ones(k, device=dev)
         bet = torch.zeros(k, device=dev)
         rm = torch.zeros(k, device=dev)
         rv = torch.ones(k, device=dev)
         sm = torch.empty(k, device=dev)
         si = torch.empty(k, device=dev)
-        stats = torch.zeros(2 * n, dtype=torch.float64, device=dev)
+        stats = torch.zeros(S * 2 * n, dtype=torch.float64, device=dev)
         for label, mode, drop, want_stats in [("raw", 0, 0.0, False), ("raw+stats", 0, 0.0, True),
                                               ("bn-train", 1, 0.0, True), ("bn-train+drop", 1, 0.2, True)]:
             a = LinearFwdArgs()
@@ -72,9 +73,9 @@ def main():
         dz = torch.empty(m, n, device=dev)
         dw = torch.zeros(n, k, device=dev)
         db = torch.zeros(n, device=dev)
-        gst = torch.zeros(2 * n, dtype=torch.float64, device=dev)
+        gst = torch.zeros(S * 2 * n, dtype=torch.float64, device=dev)
         gprev = torch.empty(m, k, device=dev)
-        gprev_st = torch.zeros(2 * k, dtype=torch.float64, device=dev)
+        gprev_st = torch.zeros(S * 2 * k, dtype=torch.float64, device=dev)
         smn = torch.zeros(n, device=dev)
         sin = torch.ones(n, device=dev)
         gn = torch.ones(n, device=dev)

@@ -18,12 +18,15 @@ def from_db(path):
     return rows
 
 
-def from_csv(path):
+def from_csv(path, by_grid=False):
     rows = []
     with open(path) as f:
         r = csv.DictReader(f)
         for d in r:
             name = d.get("Kernel_Name") or d.get("KernelName") or d.get("Name")
+            name = name.split("(")[0] if by_grid else name
+            if by_grid and "Grid_Size_X" in d:
+                name += " grid=%sx%sx%s" % (d["Grid_Size_X"], d["Grid_Size_Y"], d["Grid_Size_Z"])
             if "Start_Timestamp" in d:
                 dur = int(d["End_Timestamp"]) - int(d["Start_Timestamp"])
             else:
@@ -37,8 +40,9 @@ def main():
     ap.add_argument("src")
     ap.add_argument("--out")
     ap.add_argument("--title", default="rocprofv3 --kernel-trace summary")
+    ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size) = per launch shape")
     a = ap.parse_args()
-    rows = from_db(a.src) if a.src.endswith(".db") else from_csv(a.src)
+    rows = from_db(a.src) if a.src.endswith(".db") else from_csv(a.src, a.by_grid)
     agg = defaultdict(list)
     for name, dur in rows:
         agg[name].append(dur)
