@@ -1,0 +1,201 @@
+"""Multi-GPU paths of SURVEY §8(e): one process per GPU, torch.distributed
+(backend "nccl" = RCCL over xGMI on MI355X).
+
+* Corpus-sharded exact top-K (config C4). The reference serves one
+  ``faiss.IndexFlatIP`` per process (src/serving/retrieval.py:70-197); here the
+  corpus is row-partitioned into contiguous shards, every rank runs
+  ``rt_flatip_topk`` on the same query tile against its shard with the shard's
+  global row offset, the per-rank (score, id) lists are exchanged ONCE with
+  ``all_gather_into_tensor`` and merged by ``rt_topk_merge`` under the
+  (score desc, id asc) rule. Scores depend only on (query, row) and the
+  reduction runs over D, so the merged result is identical to one GPU holding
+  the whole corpus.
+* Table-sharded row gather (config C5): the owner of row ``id`` is the rank
+  whose contiguous range holds it; the batch ids are all-gathered, every rank
+  gathers the rows it owns into a dense buffer (zeros elsewhere, via
+  ``rt_gather_rows``' row window) and one all-reduce(sum) leaves every row on
+  every rank.
+* Data-parallel training: the flat fp32 grad slab is averaged with one
+  all-reduce (see training/fused_step.py).
+
+The orchestration functions take the per-rank compute as callables so the
+collective logic is testable on CPU with the gloo backend; the product class
+(`ShardedFlatIPIndex`) binds them to the HIP kernels only.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import kernels
+
+TopkFn = Callable[[torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]
+MergeFn = Callable[[torch.Tensor, torch.Tensor, int], Tuple[torch.Tensor, torch.Tensor]]
+
+
+def _world(group) -> Tuple[int, int]:
+    if not dist.is_available() or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous balanced row partition: (begin, count) of ``rank``'s shard;
+    the first ``n_total % world`` ranks hold one extra row."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} for world {world}")
+    base, extra = divmod(int(n_total), world)
+    begin = rank * base + min(rank, extra)
+    return begin, base + (1 if rank < extra else 0)
+
+
+def owner_of(ids: torch.Tensor, n_total: int, world: int) -> torch.Tensor:
+    """Rank owning each global row id under :func:`shard_range`."""
+    base, extra = divmod(int(n_total), world)
+    cut = extra * (base + 1)
+    ids = ids.to(torch.int64)
+    low = torch.div(ids, base + 1, rounding_mode="floor")
+    high = extra + torch.div(ids - cut, max(base, 1), rounding_mode="floor")
+    return torch.where(ids < cut, low, high)
+
+
+def all_gather_candidates(scores: torch.Tensor, ids: torch.Tensor, group=None
+                          ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """[nq, k] per rank → [world, nq, k] on every rank (two all_gather_into_tensor,
+    the only exchange step of the sharded search)."""
+    world, _ = _world(group)
+    if world == 1:
+        return scores.unsqueeze(0), ids.unsqueeze(0)
+    scores = scores.contiguous()
+    ids = ids.contiguous()
+    # concatenated along dim 0 (the layout every backend accepts), viewed [world, nq, k]
+    out_s = torch.empty((world * scores.shape[0],) + tuple(scores.shape[1:]), dtype=scores.dtype,
+                        device=scores.device)
+    out_i = torch.empty((world * ids.shape[0],) + tuple(ids.shape[1:]), dtype=ids.dtype, device=ids.device)
+    dist.all_gather_into_tensor(out_s, scores, group=group)
+    dist.all_gather_into_tensor(out_i, ids, group=group)
+    return out_s.view((world,) + tuple(scores.shape)), out_i.view((world,) + tuple(ids.shape))
+
+
+def sharded_topk(queries: torch.Tensor, k: int, local_topk: TopkFn, merge: MergeFn,
+                 group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact top-k over a row-sharded corpus. ``local_topk`` returns this rank's
+    (scores [nq,k], GLOBAL ids [nq,k]) padded with (-FLT_MAX, -1); ``merge`` maps
+    [world, nq, k] lists to the final [nq, k]. Every rank returns the result."""
+    s, i = local_topk(queries, k)
+    world, _ = _world(group)
+    if world == 1:
+        return s, i
+    all_s, all_i = all_gather_candidates(s, i, group)
+    return merge(all_s, all_i, k)
+
+
+def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Tensor, group=None,
+                        gather: Optional[Callable] = None) -> torch.Tensor:
+    """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL
+    batch (all ranks' ``ids`` concatenated in rank order) on every rank.
+
+    ``gather(table, ids, row_begin)`` must return [len(ids), dim] with zero rows
+    for ids outside this rank's window (``rt_gather_rows`` semantics, the
+    default); the all-reduce(sum) then completes every row exactly once
+    (x + 0 is exact, so the result is bit-identical to a single-table gather)."""
+    gather = gather or (lambda t, i, b: kernels.gather_rows(t, i, row_begin=b))
+    world, _ = _world(group)
+    if world == 1:
+        return gather(table_shard, ids, row_begin)
+    n_local = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
+    counts = [torch.zeros_like(n_local) for _ in range(world)]
+    dist.all_gather(counts, n_local, group=group)
+    counts = [int(c.item()) for c in counts]
+    width = max(counts)
+    padded = torch.full((width,), -1, dtype=torch.int64, device=ids.device)
+    padded[: ids.numel()] = ids.to(torch.int64)
+    all_ids = torch.empty((world * width,), dtype=torch.int64, device=ids.device)
+    dist.all_gather_into_tensor(all_ids, padded, group=group)
+    keep = torch.cat([torch.arange(r * width, r * width + c, device=ids.device) for r, c in enumerate(counts)])
+    global_ids = all_ids[keep]
+    rows = gather(table_shard, global_ids, row_begin)
+    dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=group)
+    return rows
+
+
+def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Data-parallel gradient average (one all-reduce of the flat grad slab)."""
+    world, _ = _world(group)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t.mul_(1.0 / world)
+    return t
+
+
+# ---------------------------------------------------------------------------
+class ShardedFlatIPIndex:
+    """Row-sharded exact inner-product index, one shard per rank in its GPU's HBM.
+
+    ``build(embeddings)`` takes the full corpus on every rank (each keeps its
+    slice) or ``build_shard(rows, begin, n_total)`` its own rows only. Search
+    returns GLOBAL row positions; ``metric='cosine'`` renormalises with the
+    Faiss rule (``rt_l2_renorm_f32``) before any storage cast, like the
+    single-GPU ``HipFlatIPIndex``."""
+
+    def __init__(self, dimension: int, group=None, device: Optional[torch.device] = None,
+                 storage_dtype: torch.dtype = torch.float32, metric: str = "cosine"):
+        self.dimension = dimension
+        self.group = group
+        self.world, self.rank = _world(group)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.storage_dtype = storage_dtype
+        self.metric = metric
+        self.shard: Optional[torch.Tensor] = None
+        self.begin = 0
+        self.n_total = 0
+
+    def _prep(self, x) -> torch.Tensor:
+        t = torch.as_tensor(x) if not isinstance(x, torch.Tensor) else x
+        if t.dim() == 1:
+            t = t.reshape(1, -1)
+        t = t.to(device=self.device, dtype=torch.float32, copy=True).contiguous()
+        if t.shape[1] != self.dimension:
+            raise ValueError(f"expected dimension {self.dimension}, got {t.shape[1]}")
+        if self.metric == "cosine":
+            kernels.l2_renorm_(t)
+        return t.to(self.storage_dtype)
+
+    def build_shard(self, rows, begin: int, n_total: int):
+        self.shard = self._prep(rows)
+        self.begin, self.n_total = int(begin), int(n_total)
+        return self
+
+    def build(self, embeddings):
+        n = len(embeddings)
+        b, c = shard_range(n, self.world, self.rank)
+        return self.build_shard(embeddings[b:b + c], b, n)
+
+    @property
+    def current_size(self) -> int:
+        return self.n_total
+
+    def _local(self, excluded: Optional[Sequence[Sequence[int]]]) -> TopkFn:
+        def fn(q: torch.Tensor, k: int):
+            bits = None
+            if excluded is not None:
+                n_loc = self.shard.shape[0]
+                loc = [[int(i) - self.begin for i in ex if self.begin <= int(i) < self.begin + n_loc]
+                       for ex in excluded]
+                bits = kernels.exclusion_bitmap(q.shape[0], n_loc, loc, q.device)
+            return kernels.flatip_topk(q, self.shard, k, exclude_bits=bits, id_offset=self.begin)
+        return fn
+
+    def search_tensors(self, queries, k: int, excluded: Optional[Sequence[Sequence[int]]] = None
+                       ) -> Tuple[torch.Tensor, torch.Tensor]:
+        if self.shard is None:
+            raise ValueError("Index not built yet")
+        q = self._prep(queries)
+        return sharded_topk(q, k, self._local(excluded), kernels.topk_merge, self.group)
+
+    def search(self, queries, k: int = 10) -> Tuple[np.ndarray, np.ndarray]:
+        s, i = self.search_tensors(queries, k)
+        return s.cpu().numpy(), i.cpu().numpy()

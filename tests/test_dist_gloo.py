@@ -1,0 +1,129 @@
+"""N>1 paths on CPU: world_size-2 gloo process groups driving
+the same orchestration code the GPU ranks run (src/dist/sharded.py), with the
+per-rank compute bound to the oracle (tests may use the oracle as checker).
+
+* corpus-sharded exact top-K: merged result == one index over the whole corpus,
+  bit-exact on dyadic data (ties resolved by the lower global id);
+* table-sharded gather + all-reduce == one gather from the unsharded table;
+* data-parallel gradient average.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import flat_ip as orc
+from src.dist.sharded import allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_topk
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, fn, *args):
+    port = _free_port()
+    mp.spawn(_entry, args=(world, port, fn, args), nprocs=world, join=True)
+
+
+def _entry(rank, world, port, fn, args):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world, *args)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _dyadic(rng, n, d):
+    # multiples of 2^-6 in [-1, 1]: every partial sum is exact in fp32, so any
+    # summation order gives the same bits (SURVEY §8(c) parity contract 1)
+    return (rng.integers(-64, 65, size=(n, d)) / 64.0).astype(np.float32)
+
+
+# ---------------------------------------------------------------------------
+def test_shard_range_partitions_contiguously():
+    for n in (0, 1, 7, 1000, 1001, 12_500_000 * 8 + 3):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0
+            for (b0, c0), (b1, _) in zip(spans, spans[1:]):
+                assert b0 + c0 == b1
+            assert sum(c for _, c in spans) == n
+            assert max(c for _, c in spans) - min(c for _, c in spans) <= 1
+    ids = torch.arange(1001)
+    own = owner_of(ids, 1001, 3)
+    for r in range(3):
+        b, c = shard_range(1001, 3, r)
+        assert torch.all(own[b:b + c] == r)
+
+
+def _topk_worker(rank, world, n, d, nq, k, seed, with_ties):
+    rng = np.random.default_rng(seed)
+    corpus = _dyadic(rng, n, d)
+    queries = _dyadic(rng, nq, d)
+    if with_ties:  # duplicate rows across the shard boundary: equal scores, lower id must win
+        corpus[n - 1] = corpus[0]
+        corpus[n // 2] = corpus[1]
+    b, c = shard_range(n, world, rank)
+    shard = corpus[b:b + c]
+
+    def local(q, kk):
+        s, i = orc.flat_ip_search(q.numpy(), shard, kk, id_offset=b)
+        return torch.from_numpy(s), torch.from_numpy(i)
+
+    def merge(s, i, kk):
+        ms, mi = orc.topk_merge(s.numpy(), i.numpy(), kk)
+        return torch.from_numpy(ms), torch.from_numpy(mi)
+
+    got_s, got_i = sharded_topk(torch.from_numpy(queries), k, local, merge)
+    ref_s, ref_i = orc.flat_ip_search(queries, corpus, k)
+    np.testing.assert_array_equal(got_i.numpy(), ref_i)
+    np.testing.assert_array_equal(got_s.numpy(), ref_s)
+
+
+@pytest.mark.parametrize("n,k,ties", [(1001, 10, False), (300, 100, True), (37, 50, False)])
+def test_sharded_topk_matches_single_index_gloo(n, k, ties):
+    _run(2, _topk_worker, n, 32, 19, k, 7, ties)
+
+
+def _gather_worker(rank, world, n, d, seed):
+    rng = np.random.default_rng(seed)
+    table = rng.standard_normal((n, d)).astype(np.float32)
+    counts = [13, 29]
+    all_ids = [rng.integers(0, n, size=c) for c in counts]
+    b, c = shard_range(n, world, rank)
+    shard = torch.from_numpy(table[b:b + c])
+
+    def window_gather(t, ids, begin):  # rt_gather_rows semantics: rows outside the window are zero
+        loc = ids - begin
+        ok = (loc >= 0) & (loc < t.shape[0])
+        out = torch.zeros((ids.numel(), t.shape[1]), dtype=t.dtype)
+        out[ok] = t[loc[ok]]
+        return out
+
+    rows = sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=window_gather)
+    ref = table[np.concatenate(all_ids)]
+    np.testing.assert_array_equal(rows.numpy(), ref)
+
+
+def test_sharded_gather_rows_gloo():
+    _run(2, _gather_worker, 997, 16, 3)
+
+
+def _dp_worker(rank, world):
+    g = torch.full((5,), float(rank + 1))
+    allreduce_mean_(g)
+    assert torch.all(g == 1.5)
+
+
+def test_allreduce_mean_gloo():
+    _run(2, _dp_worker)
