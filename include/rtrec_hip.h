@@ -206,6 +206,10 @@ typedef struct {
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);
+/* the two launches of rt_linear_bwd_f32, separately (same arguments, same
+ * order on one stream): dz/dgamma/dbeta/dA, then dW/dbias from dz_ws. */
+int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream);
+int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream);
 
 /* ------------------------------------------------------------------------
  * Losses (fp32 scores, fp32 accumulation; bf16/f16 inputs widened on load).

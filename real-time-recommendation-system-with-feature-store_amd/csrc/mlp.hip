@@ -705,7 +705,7 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
     return check_launch("linear_fwd_kernel");
 }
 
-extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
+static int validate_bwd(const rt_linear_bwd_args* args) {
     if (!args) return RT_ERR_INVALID;
     const rt_linear_bwd_args& a = *args;
     if (a.m < 0 || a.k <= 0 || a.n <= 0 || !a.w || !a.dw || !a.dz_ws || !a.src || a.ld_src < a.k)
@@ -720,45 +720,61 @@ extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
     if ((a.prev_mode == 1 || a.prev_mode == 2) &&
         (!a.prev_mean || !a.prev_invstd || !a.prev_gamma || !a.prev_beta))
         return RT_ERR_INVALID;
+    return RT_OK;
+}
+
+extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream) {
+    const int v = validate_bwd(args);
+    if (v) return v;
+    const rt_linear_bwd_args& a = *args;
     if (a.m == 0) return RT_OK;
     hipStream_t st = as_stream(stream);
-    {
-        const int tpwk = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
-        const int np = mlp::pad8(a.n);
-        const size_t lds = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) + 16;
-        const dim3 grid(static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM));
-        switch (tpwk) {
-            case 1: allow_lds(mlp::linear_bwd_dz_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<1>, grid, dim3(256), lds, st, a); break;
-            case 2: allow_lds(mlp::linear_bwd_dz_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<2>, grid, dim3(256), lds, st, a); break;
-            default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, a); break;
-        }
-        const int rc = check_launch("linear_bwd_dz_kernel");
-        if (rc) return rc;
+    const bool need_da = a.g_prev || a.dsrc;
+    const int tpwk = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
+    const int np = mlp::pad8(a.n);
+    const size_t lds = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) + 16;
+    const dim3 grid(static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM));
+    switch (tpwk) {
+        case 1: allow_lds(mlp::linear_bwd_dz_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<1>, grid, dim3(256), lds, st, a); break;
+        case 2: allow_lds(mlp::linear_bwd_dz_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<2>, grid, dim3(256), lds, st, a); break;
+        default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, a); break;
     }
-    {
-        const int kt = a.k <= 32 ? 1 : 2;
-        const int tn = (a.n + mlp::DW_N - 1) / mlp::DW_N;
-        const int tk = (a.k + 32 * kt - 1) / (32 * kt);
-        // ~512 blocks (2 per CU), >= 64 rows per block, <= 32 splits per tile
-        int64_t splits = (512 + tn * tk - 1) / (tn * tk);
-        const int64_t max_splits = (a.m + 63) / 64;
-        if (splits > max_splits) splits = max_splits;
-        if (splits > 32) splits = 32;
-        if (splits < 1) splits = 1;
-        int64_t rps = (a.m + splits - 1) / splits;
-        rps = (rps + 63) / 64 * 64;
-        splits = (a.m + rps - 1) / rps;
-        const dim3 grid(static_cast<unsigned>(tn), static_cast<unsigned>(tk), static_cast<unsigned>(splits));
-        int pro = 0;
-        if (a.prev_mode != 0)
-            pro = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
+    return check_launch("linear_bwd_dz_kernel");
+}
+
+extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream) {
+    const int v = validate_bwd(args);
+    if (v) return v;
+    const rt_linear_bwd_args& a = *args;
+    if (a.m == 0) return RT_OK;
+    hipStream_t st = as_stream(stream);
+    const int kt = a.k <= 32 ? 1 : 2;
+    const int tn = (a.n + mlp::DW_N - 1) / mlp::DW_N;
+    const int tk = (a.k + 32 * kt - 1) / (32 * kt);
+    // ~512 blocks (2 per CU), >= 64 rows per block, <= 32 splits per tile
+    int64_t splits = (512 + tn * tk - 1) / (tn * tk);
+    const int64_t max_splits = (a.m + 63) / 64;
+    if (splits > max_splits) splits = max_splits;
+    if (splits > 32) splits = 32;
+    if (splits < 1) splits = 1;
+    int64_t rps = (a.m + splits - 1) / splits;
+    rps = (rps + 63) / 64 * 64;
+    splits = (a.m + rps - 1) / rps;
+    const dim3 grid(static_cast<unsigned>(tn), static_cast<unsigned>(tk), static_cast<unsigned>(splits));
+    int pro = 0;
+    if (a.prev_mode != 0)
+        pro = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
 #define RT_DW(KT, P) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<KT, P>), grid, dim3(256), 0, st, a, rps)
-        if (kt == 1) {
-            switch (pro) { case 0: RT_DW(1, 0); break; case 1: RT_DW(1, 1); break; case 2: RT_DW(1, 2); break; default: RT_DW(1, 3); }
-        } else {
-            switch (pro) { case 0: RT_DW(2, 0); break; case 1: RT_DW(2, 1); break; case 2: RT_DW(2, 2); break; default: RT_DW(2, 3); }
-        }
-#undef RT_DW
-        return check_launch("linear_bwd_dw_kernel");
+    if (kt == 1) {
+        switch (pro) { case 0: RT_DW(1, 0); break; case 1: RT_DW(1, 1); break; case 2: RT_DW(1, 2); break; default: RT_DW(1, 3); }
+    } else {
+        switch (pro) { case 0: RT_DW(2, 0); break; case 1: RT_DW(2, 1); break; case 2: RT_DW(2, 2); break; default: RT_DW(2, 3); }
     }
+#undef RT_DW
+    return check_launch("linear_bwd_dw_kernel");
+}
+
+extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
+    const int rc = rt_linear_bwd_dz_f32(args, stream);
+    return rc ? rc : rt_linear_bwd_dw_f32(args, stream);
 }

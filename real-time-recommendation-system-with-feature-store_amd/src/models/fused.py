@@ -390,7 +390,11 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
             gs[li - 1] = g
             a.g_prev = g.data_ptr()
         da = a.g_prev is not None or a.dsrc is not None
-        with TIMER.region("linear_bwd", flops=(4.0 if da else 2.0) * m * a.k * a.n,
-                          bytes_=4.0 * (3 * m * a.n + m * a.k * (2 if da else 1) + 2 * a.n * a.k)):
-            call("rt_linear_bwd_f32", ctypes.byref(a), st)
+        # two launches, timed separately (bench roofline): dz (+dA) then dW (+dbias)
+        with TIMER.region("linear_bwd_dz", flops=(2.0 if da else 0.0) * m * a.k * a.n,
+                          bytes_=4.0 * (3 * m * a.n + (2 * m * a.k if da else 0) + a.n * a.k)):
+            call("rt_linear_bwd_dz_f32", ctypes.byref(a), st)
+        with TIMER.region("linear_bwd_dw", flops=2.0 * m * a.k * a.n,
+                          bytes_=4.0 * (m * a.n + m * a.k + a.n * a.k)):
+            call("rt_linear_bwd_dw_f32", ctypes.byref(a), st)
     return dsrc
