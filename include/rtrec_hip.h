@@ -98,6 +98,18 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
 int rt_topk_merge(const float* scores, const int64_t* ids, int64_t nq, int n_lists, int k_in,
                   int k_out, float* out_scores, int64_t* out_ids, void* stream);
 
+/* On-device negative sampling (sample_negative_items, src/data/movielens.py:
+ * 488-512, called per sample by src/training/datasets/movielens.py:104-108).
+ * Per row r: num_neg distinct items uniform over [0, num_items) minus the
+ * positives of user users[r] (CSR: pos_items[pos_offsets[u] .. pos_offsets[u+1])
+ * sorted ascending, unique); if that pool has <= num_neg items, the pool in
+ * increasing order followed by -1. Counter-based RNG: the draw is a pure
+ * function of (seed + *seed_offset, row, slot, round). num_neg <= 64,
+ * num_items < 2^31. out [n, num_neg] int64. */
+int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* pos_items, int64_t n_users,
+                        const int64_t* users, int64_t n, int64_t num_items, int num_neg, uint64_t seed,
+                        const uint64_t* seed_offset, int64_t* out, void* stream);
+
 /* ------------------------------------------------------------------------
  * Tower MLP (src/models/two_tower.py:56-72,98-134,196-212,238-281):
  * hidden block l = Linear → act → BatchNorm1d → Dropout, final Linear, then

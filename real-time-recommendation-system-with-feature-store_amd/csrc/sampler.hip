@@ -1,0 +1,116 @@
+// On-device negative sampling (the GPU data feeder).
+//
+// Replaces sample_negative_items (src/data/movielens.py:488-512) as called per
+// sample by MovieLensDataset.__getitem__ (src/training/datasets/movielens.py:
+// 104-108): num_negatives items drawn uniformly WITHOUT replacement from the
+// items the user has not interacted with; when that pool is smaller than
+// num_negatives the whole pool is returned (here: in increasing id order, the
+// remaining slots = -1).
+//
+// One wave per batch row. Lane j owns negative slot j: it proposes a
+// counter-hashed item, rejects it if it is one of the user's positives
+// (binary search in the user's sorted CSR segment) or equals an accepted slot or
+// a lower lane's same-round proposal, and retries until every slot holds a value.
+// Distinctness is exact; the accepted set is uniform over the pool because each
+// round's proposals are uniform and rejection only removes forbidden values.
+#include "rt_common.h"
+
+namespace rt {
+namespace sampler {
+
+constexpr int kMaxNeg = 64;
+constexpr int kMaxRounds = 4096;
+
+__device__ __forceinline__ uint32_t draw(uint64_t seed, int64_t row, int round, int j) {
+    return static_cast<uint32_t>(mix64(seed ^ (static_cast<uint64_t>(row) * 0xD1B54A32D192ED03ull) ^
+                                       (static_cast<uint64_t>(round) * 64u + static_cast<uint64_t>(j)) *
+                                           0x9E3779B97F4A7C15ull) >> 32);
+}
+
+__device__ __forceinline__ bool contains(const int32_t* __restrict__ items, int64_t lo, int64_t hi, int32_t c) {
+    int64_t a = lo, b = hi;
+    while (a < b) {
+        const int64_t mid = (a + b) >> 1;
+        if (items[mid] < c) a = mid + 1;
+        else b = mid;
+    }
+    return a < hi && items[a] == c;
+}
+
+__global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __restrict__ offsets,
+                                                               const int32_t* __restrict__ items, int64_t n_users,
+                                                               const int64_t* __restrict__ users, int64_t n,
+                                                               int64_t num_items, int num_neg, uint64_t seed,
+                                                               const uint64_t* __restrict__ seed_offset,
+                                                               int64_t* __restrict__ out) {
+    __shared__ int32_t acc_s[4][kMaxNeg];
+    __shared__ int32_t prop_s[4][kMaxNeg];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + w;
+    if (row >= n) return;
+    const uint64_t sd = seed + (seed_offset ? *seed_offset : 0ull);
+    const int64_t u = users[row];
+    int64_t lo = 0, hi = 0;
+    if (u >= 0 && u < n_users) { lo = offsets[u]; hi = offsets[u + 1]; }
+    const int64_t pool = num_items - (hi - lo);
+    int64_t* o = out + row * num_neg;
+    if (pool <= num_neg) {
+        // the whole pool in id order (reference: `return negative_pool`), -1 padded
+        int written = 0;
+        for (int64_t base = 0; base < num_items && written < num_neg; base += 64) {
+            const int64_t c = base + lane;
+            const bool keep = c < num_items && !contains(items, lo, hi, static_cast<int32_t>(c));
+            const uint64_t m = __ballot(keep);
+            const int before = __popcll(m & ((1ull << lane) - 1ull));
+            if (keep && written + before < num_neg) o[written + before] = c;
+            written += __popcll(m);
+        }
+        for (int j = (written < num_neg ? written : num_neg) + lane; j < num_neg; j += 64) o[j] = -1;
+        return;
+    }
+    int32_t mine = -1;
+    const bool active = lane < num_neg;
+    if (lane < kMaxNeg) acc_s[w][lane] = -1;
+    for (int round = 0; round < kMaxRounds; ++round) {
+        const bool want = active && mine < 0;
+        if (!__ballot(want)) break;
+        int32_t c = -1;
+        if (want) {
+            const uint32_t r = draw(sd, row, round, lane);
+            c = static_cast<int32_t>((static_cast<uint64_t>(r) * static_cast<uint64_t>(num_items)) >> 32);
+        }
+        if (lane < kMaxNeg) prop_s[w][lane] = c;
+        wave_lds_sync();
+        bool ok = want && !contains(items, lo, hi, c);
+        if (ok) {
+            for (int j = 0; j < num_neg; ++j) {
+                if (acc_s[w][j] == c || (j < lane && prop_s[w][j] == c)) { ok = false; break; }
+            }
+        }
+        wave_lds_sync();
+        if (ok) {
+            mine = c;
+            acc_s[w][lane] = c;
+        }
+        wave_lds_sync();
+    }
+    if (active) o[lane] = mine;  // -1 only if kMaxRounds ran out (pool > num_neg makes that vanishing)
+}
+
+}  // namespace sampler
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* pos_items, int64_t n_users,
+                                   const int64_t* users, int64_t n, int64_t num_items, int num_neg, uint64_t seed,
+                                   const uint64_t* seed_offset, int64_t* out, void* stream) {
+    if (n < 0 || n_users < 0 || num_items <= 0 || num_items >= (1ll << 31) || num_neg <= 0) return RT_ERR_INVALID;
+    if (num_neg > sampler::kMaxNeg) return RT_ERR_UNSUPPORTED;
+    if (n == 0) return RT_OK;
+    if (!pos_offsets || !users || !out || (!pos_items && n_users > 0)) return RT_ERR_INVALID;
+    const dim3 grid(static_cast<unsigned>((n + 3) / 4));
+    hipLaunchKernelGGL(sampler::sample_negatives_kernel, grid, dim3(256), 0, as_stream(stream), pos_offsets,
+                       pos_items, n_users, users, n, num_items, num_neg, seed, seed_offset, out);
+    return check_launch("sample_negatives_kernel");
+}

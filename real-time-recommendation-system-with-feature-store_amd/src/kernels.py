@@ -152,3 +152,21 @@ def exclusion_bitmap(n_queries: int, n_items: int, excluded, device) -> torch.Te
             mask[q, sel] = True
     packed = np.packbits(mask, axis=1, bitorder="little")  # little-endian words: bit j = item j
     return torch.from_numpy(np.ascontiguousarray(packed).view(np.int32).copy()).to(device)
+
+
+def sample_negatives(pos_offsets: torch.Tensor, pos_items: torch.Tensor, users: torch.Tensor, num_items: int,
+                     num_neg: int, seed: int, seed_offset: Optional[torch.Tensor] = None,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[n, num_neg] int64 negatives per row (rt_sample_negatives): distinct, uniform
+    over the items user ``users[r]`` has not interacted with (CSR positives)."""
+    native.require_device(pos_offsets, pos_items, users, what="sample_negatives")
+    if pos_offsets.dtype != torch.int64 or pos_items.dtype != torch.int32:
+        raise TypeError("CSR must be int64 offsets and int32 sorted items")
+    users = users.contiguous().to(torch.int64)
+    n = users.numel()
+    if out is None:
+        out = torch.empty((n, num_neg), dtype=torch.int64, device=users.device)
+    with TIMER.region("sample_negatives", bytes_=8.0 * n * (num_neg + 1)):
+        call("rt_sample_negatives", ptr(pos_offsets), ptr(pos_items), pos_offsets.numel() - 1, ptr(users), n,
+             num_items, num_neg, seed & 0xFFFFFFFFFFFFFFFF, ptr(seed_offset), ptr(out), stream_of(users))
+    return out

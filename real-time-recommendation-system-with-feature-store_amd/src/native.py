@@ -78,6 +78,7 @@ SIGNATURES = {
     "rt_flatip_topk": (c_int, [vp, c_i64, vp, c_i64, c_int, c_int, c_int, vp, c_i64, c_i64, vp, vp, vp,
                                c_size, vp]),
     "rt_topk_merge": (c_int, [vp, vp, c_i64, c_int, c_int, c_int, vp, vp, vp]),
+    "rt_sample_negatives": (c_int, [vp, vp, c_i64, vp, c_i64, c_i64, c_int, c_u64, vp, vp, vp]),
     "rt_linear_fwd_f32": (c_int, [ctypes.POINTER(LinearFwdArgs), vp]),
     "rt_linear_bwd_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_bwd_dz_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),

@@ -68,6 +68,37 @@ class FusedTrainStep:
         self.lr = lr
         self.lr_dev.fill_(lr)
 
+    def optimizer_state_dict(self) -> dict:
+        """The Adam state in torch.optim.Adam.state_dict() layout (params indexed
+        in model.parameters() order), so checkpoints read like the reference's
+        (src/training/trainers/two_tower.py:199)."""
+        step = float(self.step_dev.item())
+        state = {}
+        for i, (o, e) in enumerate(self.slab.bounds):
+            shape = self.slab.params[i].shape
+            state[i] = {"step": torch.tensor(step), "exp_avg": self.exp_avg[o:e].view(shape).clone(),
+                        "exp_avg_sq": self.exp_avg_sq[o:e].view(shape).clone()}
+        group = {"lr": self.lr, "betas": (self.b1, self.b2), "eps": self.eps, "weight_decay": self.wd,
+                 "amsgrad": False, "maximize": False, "foreach": None, "capturable": False,
+                 "differentiable": False, "fused": None, "params": list(range(len(self.slab.params)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd: dict):
+        """Inverse of optimizer_state_dict (also accepts a reference Adam state dict)."""
+        steps = set()
+        for i, (o, e) in enumerate(self.slab.bounds):
+            st = sd["state"].get(i, sd["state"].get(str(i)))
+            if st is None:
+                continue
+            self.exp_avg[o:e].copy_(st["exp_avg"].reshape(-1))
+            self.exp_avg_sq[o:e].copy_(st["exp_avg_sq"].reshape(-1))
+            steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError("per-parameter Adam step counts differ; the fused step keeps one counter")
+        if steps:
+            self.step_dev.fill_(steps.pop())
+        self.set_lr(float(sd["param_groups"][0]["lr"]))
+
     # ------------------------------------------------------------------
     def _run(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None):
         m = self.model

@@ -1,0 +1,156 @@
+"""TwoTowerTrainer (reference src/training/trainers/two_tower.py:25-273) on the
+fused MI355X step.
+
+Same constructor, config keys, schedule and bookkeeping as the reference:
+Adam(lr, weight_decay), ReduceLROnPlateau(mode=min, factor=0.5, patience=2) on
+the validation loss, early stopping, ``two_tower_latest.pth`` /
+``two_tower_best.pth`` checkpoints with the reference's keys. The inner step —
+three tower calls, 0.7·contrastive + 0.3·in-batch, backward,
+clip_grad_norm_(1.0), Adam — is ``FusedTrainStep`` (one fixed launch sequence,
+no autograd). Batches are either the reference's feature dicts
+(``user_features``, ``pos_item_features``, ``neg_item_features``) or the id
+batches of ``DeviceFeeder`` (``user_ids``/``pos_ids``/``neg_ids`` + tables).
+Per-batch losses are accumulated on the device; the host reads one number
+per epoch.
+"""
+from __future__ import annotations
+
+import time
+from pathlib import Path
+from typing import Any, Dict, Iterable, List
+
+import torch
+
+from ... import kernels
+from ...models.two_tower import TwoTowerModel
+from ..fused_step import FusedTrainStep
+
+
+class _ReduceLROnPlateau:
+    """torch.optim.lr_scheduler.ReduceLROnPlateau(mode='min', factor, patience)
+    with torch's defaults (threshold 1e-4 relative, cooldown 0, min_lr 0, eps 1e-8)."""
+
+    def __init__(self, step: FusedTrainStep, factor: float = 0.5, patience: int = 2, threshold: float = 1e-4,
+                 eps: float = 1e-8):
+        self.step, self.factor, self.patience, self.threshold, self.eps = step, factor, patience, threshold, eps
+        self.best = float("inf")
+        self.num_bad = 0
+
+    def state_dict(self):
+        return {"best": self.best, "num_bad_epochs": self.num_bad}
+
+    def __call__(self, metric: float):
+        if metric < self.best * (1.0 - self.threshold):
+            self.best = metric
+            self.num_bad = 0
+        else:
+            self.num_bad += 1
+        if self.num_bad > self.patience:
+            new_lr = self.step.lr * self.factor
+            if self.step.lr - new_lr > self.eps:
+                self.step.set_lr(new_lr)
+            self.num_bad = 0
+
+
+class TwoTowerTrainer:
+    def __init__(self, model: TwoTowerModel, train_loader: Iterable, val_loader: Iterable,
+                 config: Dict[str, Any], device: str = "cuda"):
+        self.model = model.to(device)
+        self.train_loader = train_loader
+        self.val_loader = val_loader
+        self.config = config
+        self.device = torch.device(device)
+        self.step = FusedTrainStep(model, lr=config.get("learning_rate", 0.001),
+                                   weight_decay=config.get("weight_decay", 1e-5),
+                                   max_norm=config.get("max_grad_norm", 1.0))
+        self.scheduler = _ReduceLROnPlateau(self.step, factor=0.5, patience=2)
+        self.early_stopping_patience = config.get("early_stopping_patience", 5)
+        self.best_val_loss = float("inf")
+        self.patience_counter = 0
+        self.checkpoint_dir = Path(config.get("checkpoint_dir", "models/checkpoints"))
+        self.checkpoint_dir.mkdir(parents=True, exist_ok=True)
+        self.train_losses: List[float] = []
+        self.val_losses: List[float] = []
+
+    # ------------------------------------------------------------------
+    def _run_step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        dev = self.device
+        if "user_ids" in batch:
+            return self.step(batch["user_table"], batch["item_table"],
+                             batch["item_table"] if "neg_ids" in batch else None,
+                             user_ids=batch["user_ids"], pos_ids=batch["pos_ids"], neg_ids=batch.get("neg_ids"))
+        neg = batch.get("neg_item_features")
+        return self.step(batch["user_features"].to(dev), batch["pos_item_features"].to(dev),
+                         neg.to(dev) if neg is not None else None)
+
+    def train_epoch(self, epoch: int) -> float:
+        """two_tower.py:84-156 (mixed loss when negatives are present, else in-batch only)."""
+        self.model.train()
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        n = 0
+        for batch in self.train_loader:
+            total += self._run_step(batch)[0]
+            n += 1
+        avg = float(total.item()) / n if n else 0.0
+        self.train_losses.append(avg)
+        return avg
+
+    @torch.no_grad()
+    def validate(self) -> float:
+        """two_tower.py:158-188: in-batch loss on positives, eval mode."""
+        self.model.eval()
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        n = 0
+        for batch in self.val_loader:
+            if "user_ids" in batch:
+                uf = kernels.gather_rows(batch["user_table"], batch["user_ids"])
+                pf = kernels.gather_rows(batch["item_table"], batch["pos_ids"])
+            else:
+                uf = batch["user_features"].to(self.device)
+                pf = batch["pos_item_features"].to(self.device)
+            u = self.model.get_user_embeddings({"numerical": uf, "categorical": {}})
+            p = self.model.get_item_embeddings({"numerical": pf, "categorical": {}})
+            total += self.model.in_batch_negative_loss(u, p).double()
+            n += 1
+        avg = float(total.item()) / n if n else 0.0
+        self.val_losses.append(avg)
+        return avg
+
+    def save_checkpoint(self, epoch: int, is_best: bool = False) -> None:
+        """two_tower.py:190-215 (same keys; optimizer_state in torch.optim.Adam format)."""
+        ckpt = {
+            "epoch": epoch,
+            "user_tower_state": self.model.user_tower.state_dict(),
+            "item_tower_state": self.model.item_tower.state_dict(),
+            "temperature": self.model.temperature,
+            "user_bias": self.model.user_bias,
+            "item_bias": self.model.item_bias,
+            "optimizer_state": self.step.optimizer_state_dict(),
+            "train_losses": self.train_losses,
+            "val_losses": self.val_losses,
+        }
+        torch.save(ckpt, self.checkpoint_dir / "two_tower_latest.pth")
+        if is_best:
+            torch.save(ckpt, self.checkpoint_dir / "two_tower_best.pth")
+
+    def train(self, num_epochs: int) -> None:
+        """two_tower.py:217-262."""
+        for epoch in range(1, num_epochs + 1):
+            start = time.time()
+            train_loss = self.train_epoch(epoch)
+            val_loss = self.validate()
+            self.scheduler(val_loss)
+            self.epoch_log = {"epoch": epoch, "train_loss": train_loss, "val_loss": val_loss,
+                              "seconds": time.time() - start}
+            is_best = val_loss < self.best_val_loss
+            if is_best:
+                self.best_val_loss = val_loss
+                self.patience_counter = 0
+            else:
+                self.patience_counter += 1
+            self.save_checkpoint(epoch, is_best)
+            if self.patience_counter >= self.early_stopping_patience:
+                break
+
+    def get_training_history(self) -> Dict[str, List[float]]:
+        return {"train_losses": self.train_losses, "val_losses": self.val_losses}
