@@ -65,19 +65,17 @@ int launch_merge(const float* s, const int64_t* ids, int64_t nq, int n_lists, in
     return check_launch("topk_merge_kernel");
 }
 
-inline int cap_for(int k) {
-    int c = 128;
-    while (c < k + kNT) c <<= 1;
-    return c;
+inline Shape shape_for(int dtype, int d, int k) {
+    return dtype == RT_F32 ? shape_f32(d, k) : dtype == RT_F16 ? shape_f16(d, k) : shape_bf16(d, k);
 }
 
-inline Plan make_plan(int64_t nq, int64_t nx, int k) {
+inline Plan make_plan(int64_t nq, int64_t nx, int k, const Shape& sh) {
     Plan p{};
     p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
     if (p.chunk < 1) p.chunk = 1;
-    p.q_tiles = static_cast<int>((p.chunk + kQT - 1) / kQT);
-    // enough blocks to fill 256 CUs ~2x, but keep >= 4 item tiles per split
-    const int64_t tiles = (nx + kNT - 1) / kNT;
+    p.q_tiles = static_cast<int>((p.chunk + sh.qt - 1) / sh.qt);
+    // ~2 blocks per CU (512), but keep >= 4 item tiles per split
+    const int64_t tiles = (nx + sh.nt - 1) / sh.nt;
     int64_t splits = (512 + p.q_tiles - 1) / p.q_tiles;
     int64_t max_splits = tiles / 4;
     if (max_splits < 1) max_splits = 1;
@@ -86,10 +84,10 @@ inline Plan make_plan(int64_t nq, int64_t nx, int k) {
     if (splits < 1) splits = 1;
     int64_t tiles_per = (tiles + splits - 1) / splits;
     if (tiles_per < 1) tiles_per = 1;
-    p.items_per_split = tiles_per * kNT;
+    p.items_per_split = tiles_per * sh.nt;
     p.splits = static_cast<int>(nx > 0 ? (nx + p.items_per_split - 1) / p.items_per_split : 1);
-    p.cap = cap_for(k);
-    p.cand_bytes = static_cast<size_t>(p.splits) * p.q_tiles * kQT * p.cap * sizeof(Cand);
+    p.cap = sh.cap;
+    p.cand_bytes = static_cast<size_t>(p.splits) * p.q_tiles * sh.qt * p.cap * sizeof(Cand);
     p.part_bytes = p.splits > 1 ? static_cast<size_t>(p.splits) * p.chunk * k * (sizeof(float) + sizeof(int64_t)) : 0;
     return p;
 }
@@ -102,10 +100,9 @@ inline size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 using namespace rt;
 
 extern "C" size_t rt_flatip_topk_workspace_bytes(int64_t nq, int64_t nx, int d, int dtype, int k) {
-    (void)d;
-    (void)dtype;
-    if (nq <= 0 || k <= 0 || k > topk::kMaxK) return 256;
-    const topk::Plan p = topk::make_plan(nq, nx, k);
+    if (nq <= 0 || k <= 0 || k > topk::kMaxK || d <= 0) return 256;
+    if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return 256;
+    const topk::Plan p = topk::make_plan(nq, nx, k, topk::shape_for(dtype, d, k));
     return topk::align256(p.cand_bytes) + p.part_bytes + 256;
 }
 
@@ -122,7 +119,7 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     if (nx >= 0xFFFFFFFFll || (id_offset + nx) >= 0xFFFFFFFFll || id_offset < 0) return RT_ERR_UNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(queries) | reinterpret_cast<uintptr_t>(items)) & 15) return RT_ERR_INVALID;
     if (exclude_bits && exclude_words < (nx + 31) / 32) return RT_ERR_INVALID;
-    const topk::Plan p = topk::make_plan(nq, nx, k);
+    const topk::Plan p = topk::make_plan(nq, nx, k, topk::shape_for(dtype, d, k));
     const size_t cand_al = topk::align256(p.cand_bytes);
     if (!workspace || workspace_bytes < cand_al + p.part_bytes) return RT_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);

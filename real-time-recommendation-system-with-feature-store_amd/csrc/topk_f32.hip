@@ -4,12 +4,27 @@
 namespace rt {
 namespace topk {
 
+// MFMA k-steps (2 per instruction) padded to 16 / 32 / 64 (d <= 32 / 64 / 128)
+static int s_f32(int d) {
+    const int s = (d + 1) / 2;
+    return s <= 16 ? 16 : s <= 32 ? 32 : s <= 64 ? 64 : 0;
+}
+
 int launch_f32(const Args& a, const Plan& p, hipStream_t st) {
-    const int s = (a.d + 2 - 1) / 2;  // MFMA k-steps
-    if (s <= 16) return launch_S<float, 16>(a, p, st);
-    if (s <= 32) return launch_S<float, 32>(a, p, st);
-    if (s <= 64) return launch_S<float, 64>(a, p, st);
-    return RT_ERR_UNSUPPORTED;
+    switch (s_f32(a.d)) {
+        case 16: return launch_S<float, 16>(a, p, st);
+        case 32: return launch_S<float, 32>(a, p, st);
+        case 64: return launch_S<float, 64>(a, p, st);
+        default: return RT_ERR_UNSUPPORTED;
+    }
+}
+
+Shape shape_f32(int d, int k) {
+    switch (s_f32(d)) {
+        case 16: return shape_S<float, 16>(k);
+        case 32: return shape_S<float, 32>(k);
+        default: return shape_S<float, 64>(k);
+    }
 }
 
 }  // namespace topk

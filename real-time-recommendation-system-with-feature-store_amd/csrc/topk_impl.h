@@ -4,18 +4,23 @@
 // Replaces faiss.IndexFlatIP.search (src/serving/retrieval.py:96-98,171) and
 // the masked np.dot + argsort of scripts/evaluate_model.py:217-232.
 //
-// * block = 4 waves; wave w owns 32 queries. The MFMA is oriented ITEMS × QUERIES
-//   (A = item rows from LDS, B = query fragments held in registers), so each
-//   lane's accumulator column is ONE query: its running k-th-best threshold is
-//   a per-lane register and the filter is one v_cmp per score.
-// * items stream through LDS in 64-row tiles (register-prefetched one tile ahead);
-//   32x32 MFMA sub-tiles (fp32: v_mfma_f32_32x32x2_f32 — a sequential fmaf chain
-//   over d, bit-exact vs oracle/flatip.c; f16/bf16: v_mfma_f32_32x32x16_*).
-// * a score above the query's threshold is appended to the query's candidate
-//   buffer (global workspace, L2-resident); when a buffer nears capacity the
-//   owning wave compacts it (LDS bitonic sort) and raises the threshold to the
-//   new k-th score. Items are scanned in id order and the insert is strict (>),
-//   so the lower id wins exact ties, as in Faiss's heap.
+// * block = 4 waves; wave w owns QS sets of 32 queries. The MFMA is oriented
+//   ITEMS × QUERIES (A = item rows from LDS, B = query fragments held in
+//   registers for the whole scan), so each lane's accumulator column is ONE
+//   query and every A fragment read from LDS feeds QS MFMAs.
+// * items stream through LDS in NT-row tiles, register-prefetched one tile
+//   ahead; 32x32 MFMA sub-tiles (fp32: v_mfma_f32_32x32x2_f32 — a sequential
+//   fmaf chain over d, bit-exact vs oracle/flatip.c; f16/bf16:
+//   v_mfma_f32_32x32x16_*).
+// * selection, per lane (= per query, per wave half): the 16 scores of a
+//   sub-tile are max-reduced and compared with the lane's threshold first, so
+//   a sub-tile with no candidate in the whole wave costs ~16 VALU ops; a
+//   sorted top-K list (K = 16 or 32 >= k) lives in registers, insertion by K
+//   compare-swaps; the two wave halves' lists are merged by a bitonic merge at
+//   the end. Ties are broken by id (lower id first), as in Faiss's heap.
+// * this register-list kernel serves fp32 with k <= 32 (C3 / serving: the
+//   64-cycle fp32 MFMAs of a sub-tile hide the insertion work); 16-bit scans
+//   and larger k use the candidate-buffer kernel of topk_v1.h.
 #pragma once
 
 #include <float.h>
@@ -27,8 +32,6 @@ namespace rt {
 namespace topk {
 
 constexpr int kWaves = 4;
-constexpr int kQT = 32 * kWaves;   // queries per block
-constexpr int kNT = 64;            // items per LDS tile
 constexpr int kMaxK = 512;
 constexpr int kMaxCap = 1024;
 constexpr int64_t kQueryChunk = 1 << 16;  // queries per launch (bounds the workspace)
@@ -70,12 +73,30 @@ __device__ __forceinline__ typename Mfma<T>::frag frag_from(const T* p) {
     }
 }
 
+// compile-time shape of one instantiation
+template <typename T, int S, int MODE>  // MODE = K, the register list length
+struct Cfg {
+    static constexpr int KK = Mfma<T>::kK;
+    static constexpr int DP = S * KK;                                           // padded d
+    static constexpr int QREGS = S * static_cast<int>(sizeof(typename Mfma<T>::frag) / 4);  // per query set
+    static constexpr int LREGS = 2 * MODE;                                     // register list
+    // query sets per wave: fragments + lists within ~128 VGPRs
+    static constexpr int QS_RAW = 128 / (QREGS + LREGS);
+    static constexpr int QS = QS_RAW >= 4 ? 4 : (QS_RAW >= 2 ? 2 : 1);
+    static constexpr int QT = 32 * QS * kWaves;                                // queries per block
+    static constexpr int NT = 64;                                              // items per LDS tile
+    static constexpr int VEC = 16 / static_cast<int>(sizeof(T));               // elements per 16 B
+    static constexpr int LS = DP + VEC;                                        // +16 B pad per row
+    static constexpr int TILE_VECS = NT * (DP / VEC);
+    static constexpr int LOADS = (TILE_VECS + 255) / 256;
+};
+
 struct Plan {
     int64_t chunk;       // queries per launch
     int q_tiles;         // blocks along queries per launch
     int splits;          // blocks along items
     int64_t items_per_split;
-    int cap;             // candidate buffer entries per query
+    int cap;             // candidate buffer entries per query (v1 kernel), else 0
     size_t cand_bytes, part_bytes;
 };
 
@@ -85,81 +106,67 @@ struct Args {
     Cand* cand; float* out_s; int64_t* out_i; int64_t id_offset;
 };
 
-// per-wave LDS scratch for compaction: kMaxCap candidates
-template <typename T, int S>
-struct Smem {
-    static constexpr int DP = S * Mfma<T>::kK;
-    static constexpr int LS = DP + 16 / static_cast<int>(sizeof(T));  // +16 B pad per row
-    T tile[kNT * LS];
-    Cand sortbuf[kWaves][kMaxCap];
-    int cnt[kQT];
-    float theta[kQT];
-};
+__device__ __forceinline__ int tile_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
-// compact query buffer `buf` (n entries, n <= cap) down to its top-k
-__device__ inline void wave_compact(Cand* __restrict__ buf, int n, int k, Cand* sb, int& cnt_out,
-                                    float& theta_out) {
-    const int lane = threadIdx.x & 63;
-    const int np = next_pow2(n > 64 ? n : 64);
-    for (int e = lane; e < np; e += 64) sb[e] = e < n ? buf[e] : Cand{-INFINITY, kEmptyId};
-    wave_lds_sync();
-    wave_sort_lds(sb, np);
-    const int keep = n < k ? n : k;
-    for (int e = lane; e < keep; e += 64) buf[e] = sb[e];
-    cnt_out = keep;
-    theta_out = keep == k ? sb[k - 1].s : -INFINITY;
-    wave_lds_sync();
+// insert (cs, ci) into a sorted (better-first) register list of K entries
+template <int K>
+__device__ __forceinline__ void list_insert(float (&ls)[K], uint32_t (&li)[K], float cs, uint32_t ci) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+        const bool b = better(cs, ci, ls[i], li[i]);
+        const float ts = ls[i];
+        const uint32_t ti = li[i];
+        ls[i] = b ? cs : ts;
+        li[i] = b ? ci : ti;
+        cs = b ? ts : cs;
+        ci = b ? ti : ci;
+    }
 }
 
-template <typename T, int S>
-__global__ __launch_bounds__(256) void flatip_topk_kernel(Args a, int cap, int64_t items_per_split) {
+template <typename T, int S, int K>
+__global__ __launch_bounds__(256) void flatip_topk_kernel(Args a, int64_t items_per_split) {
     using M = Mfma<T>;
-    using SM = Smem<T, S>;
-    constexpr int KK = M::kK;
-    constexpr int DP = SM::DP;
-    constexpr int LS = SM::LS;
-    constexpr int VEC = 16 / static_cast<int>(sizeof(T));  // elements per 16-byte load
-    constexpr int TILE_VECS = kNT * (DP / VEC);
-    constexpr int LOADS = (TILE_VECS + 255) / 256;
-    __shared__ SM sm;
+    using C = Cfg<T, S, K>;
+    constexpr int KK = C::KK, QS = C::QS, QT = C::QT, NT = C::NT, LS = C::LS, VEC = C::VEC, DP = C::DP;
+    constexpr int TILE_VECS = C::TILE_VECS, LOADS = C::LOADS;
+    __shared__ __attribute__((aligned(16))) T tile[NT * LS];
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
     const T* __restrict__ X = reinterpret_cast<const T*>(a.X);
     const int d = a.d, k = a.k;
     const int64_t nq = a.nq;
-    const int tid = threadIdx.x;
-    const int wave = tid >> 6;
-    const int lane = tid & 63;
-    const int col = lane & 31;          // query column inside the wave
-    const int half = lane >> 5;         // k half inside an MFMA step
-    const int ql = wave * 32 + col;     // block-local query
-    const int64_t q = static_cast<int64_t>(blockIdx.x) * kQT + ql;
-    const bool q_ok = q < nq;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    const int64_t qb = static_cast<int64_t>(blockIdx.x) * QT + wave * 32 * QS;  // wave's first query
     const int split = blockIdx.y;
     const int64_t i_begin = static_cast<int64_t>(split) * items_per_split;
     const int64_t i_end = (i_begin + items_per_split) < a.nx ? (i_begin + items_per_split) : a.nx;
     const int row_vecs = d / VEC;
 
-    // ---- query fragments in registers: B[k][query] ----
-    typename M::frag qf[S];
-    {
-        const T* qrow = Q + (q_ok ? q : 0) * d;
+    // ---- query fragments in registers: B[k][query]; per-lane top-K lists ----
+    typename M::frag qf[QS][S];
+    bool qok[QS];
+    const uint32_t* excl[QS];
+    float th[QS];
+    float ls[QS][K];
+    uint32_t li[QS][K];
+#pragma unroll
+    for (int j = 0; j < QS; ++j) {
+        const int64_t q = qb + j * 32 + col;
+        qok[j] = q < nq;
+        const T* qrow = Q + (qok[j] ? q : 0) * d;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int k0 = (KK == 2) ? (2 * s + half) : (16 * s + 8 * half);
-            if (q_ok && k0 < d) qf[s] = frag_from<T>(qrow + k0);
-            else qf[s] = typename M::frag{};
+            if (qok[j] && k0 < d) qf[j][s] = frag_from<T>(qrow + k0);
+            else qf[j][s] = typename M::frag{};
         }
+        excl[j] = (a.excl && qok[j]) ? a.excl + q * a.excl_words : nullptr;
+        th[j] = qok[j] ? -INFINITY : INFINITY;
+#pragma unroll
+        for (int i = 0; i < K; ++i) { ls[j][i] = -INFINITY; li[j][i] = kEmptyId; }
     }
-    Cand* my_cand = a.cand + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * kQT * cap;
-    Cand* my_sb = sm.sortbuf[wave];
-    if (tid < kQT) {
-        sm.cnt[tid] = 0;
-        sm.theta[tid] = (static_cast<int64_t>(blockIdx.x) * kQT + tid < nq) ? -INFINITY : INFINITY;
-    }
-    const uint32_t* my_excl = (a.excl && q_ok) ? a.excl + q * a.excl_words : nullptr;
 
-    // register prefetch of one tile (rows t0 .. t0+63, zero padded)
+    // register prefetch of one tile (rows t0 .. t0+NT-1, zero padded)
     uint4 pre[LOADS];
     auto fetch = [&](int64_t t0) {
 #pragma unroll
@@ -175,90 +182,164 @@ __global__ __launch_bounds__(256) void flatip_topk_kernel(Args a, int cap, int64
     };
     fetch(i_begin);
 
-    for (int64_t t0 = i_begin; t0 < i_end; t0 += kNT) {
-        __syncthreads();  // previous tile consumed; cnt/theta published
+    for (int64_t t0 = i_begin; t0 < i_end; t0 += NT) {
+        __syncthreads();  // previous tile consumed
 #pragma unroll
         for (int l = 0; l < LOADS; ++l) {
             const int e = tid + l * 256;
             if (e < TILE_VECS) {
                 const int r = e / (DP / VEC);
                 const int c = e % (DP / VEC);
-                *reinterpret_cast<uint4*>(sm.tile + r * LS + c * VEC) = pre[l];
+                *reinterpret_cast<uint4*>(tile + r * LS + c * VEC) = pre[l];
             }
         }
         __syncthreads();
-        if (t0 + kNT < i_end) fetch(t0 + kNT);  // overlaps the MFMA work below
-        const float th = sm.theta[ql];
+        if (t0 + NT < i_end) fetch(t0 + NT);  // overlaps the MFMA work below
+#pragma unroll 1
+        for (int rt = 0; rt < NT / 32; ++rt) {
+            const int64_t sub0 = t0 + rt * 32;
+            if (sub0 >= i_end) break;  // block-uniform
+            f32x16 acc[QS];
 #pragma unroll
-        for (int rt = 0; rt < kNT / 32; ++rt) {
-            f32x16 acc = {};
-            const T* arow = sm.tile + (rt * 32 + col) * LS + ((KK == 2) ? half : 8 * half);
+            for (int j = 0; j < QS; ++j) acc[j] = f32x16{};
+            const T* arow = tile + (rt * 32 + col) * LS + ((KK == 2) ? half : 8 * half);
 #pragma unroll
-            for (int s = 0; s < S; ++s) acc = M::run(frag_from<T>(arow + s * KK), qf[s], acc);
-            // acc[r] = score(item row (r&3)+8(r>>2)+4*half of the sub-tile, query col)
+            for (int s = 0; s < S; ++s) {
+                const typename M::frag af = frag_from<T>(arow + s * KK);
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float v = acc[r];
-                const int64_t item = t0 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-                if (v > th && item < i_end) {
-                    const bool skip = my_excl && ((my_excl[item >> 5] >> (item & 31)) & 1u);
-                    if (!skip) {
-                        const int slot = atomicAdd(&sm.cnt[ql], 1);
-                        my_cand[ql * cap + slot] = Cand{v, static_cast<uint32_t>(item)};
+                for (int j = 0; j < QS; ++j) acc[j] = M::run(af, qf[j][s], acc[j]);
+            }
+            if (sub0 + 32 > i_end) {  // partial last sub-tile: rows past the end never qualify
+                const int left = static_cast<int>(i_end - sub0);
+#pragma unroll
+                for (int j = 0; j < QS; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (tile_row(r, half) >= left) acc[j][r] = -INFINITY;
+            }
+#pragma unroll
+            for (int j = 0; j < QS; ++j) {
+                float mx = acc[j][0];
+#pragma unroll
+                for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[j][r]);
+                if (__ballot(mx > th[j]) == 0) continue;  // wave-uniform skip
+                const f32x16 aj = acc[j];
+                // rolled on purpose (one copy of the insertion code; dynamic extract)
+#pragma unroll 1
+                for (int r = 0; r < 16; ++r) {
+                    const float v = aj[r];
+                    if (v > th[j]) {
+                        const uint32_t item = static_cast<uint32_t>(sub0 + tile_row(r, half));
+                        if (excl[j] && ((excl[j][item >> 5] >> (item & 31)) & 1u)) continue;
+                        list_insert<K>(ls[j], li[j], v, item);
+                        th[j] = ls[j][K - 1];
                     }
                 }
             }
         }
-        __threadfence_block();
-        // ---- compaction of this wave's queries whose buffer nears capacity ----
-        const bool need = (lane < 32) && (sm.cnt[ql] > cap - kNT);
-        uint64_t mask = __ballot(need);
-        while (mask) {
-            const int c = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            const int qq = wave * 32 + c;
-            int nc;
-            float nt;
-            wave_compact(my_cand + qq * cap, sm.cnt[qq], k, my_sb, nc, nt);
-            __threadfence_block();
-            if (lane == 0) { sm.cnt[qq] = nc; sm.theta[qq] = nt; }
-            __threadfence_block();
-        }
     }
-    __syncthreads();
-    // ---- final selection for this wave's 32 queries ----
+
+    // ---- merge the two wave halves' lists, write this split's top-k ----
     float* os = a.out_s + static_cast<int64_t>(split) * nq * k;
     int64_t* oi = a.out_i + static_cast<int64_t>(split) * nq * k;
-    for (int c = 0; c < 32; ++c) {
-        const int qq = wave * 32 + c;
-        const int64_t gq = static_cast<int64_t>(blockIdx.x) * kQT + qq;
-        if (gq >= nq) break;
-        const int n = sm.cnt[qq];
-        const int np = next_pow2((n > k ? n : k) > 64 ? (n > k ? n : k) : 64);
-        for (int e = lane; e < np; e += 64) my_sb[e] = e < n ? my_cand[qq * cap + e] : Cand{-INFINITY, kEmptyId};
-        wave_lds_sync();
-        wave_sort_lds(my_sb, np);
-        for (int e = lane; e < k; e += 64) {
-            const Cand cv = my_sb[e];
-            const bool ok = cv.i != kEmptyId;
-            os[gq * k + e] = ok ? cv.s : -FLT_MAX;
-            oi[gq * k + e] = ok ? static_cast<int64_t>(cv.i) + a.id_offset : -1;
+#pragma unroll
+    for (int j = 0; j < QS; ++j) {
+        // elementwise best of mine[i] vs theirs[K-1-i] is a bitonic sequence
+        // holding the top K of the union; a bitonic merge sorts it
+        float ms[K];
+        uint32_t mi[K];
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const float s2 = __shfl_xor(ls[j][K - 1 - i], 32, 64);
+            const uint32_t i2 = static_cast<uint32_t>(__shfl_xor(static_cast<int>(li[j][K - 1 - i]), 32, 64));
+            const bool mine = better(ls[j][i], li[j][i], s2, i2);
+            ms[i] = mine ? ls[j][i] : s2;
+            mi[i] = mine ? li[j][i] : i2;
         }
-        wave_lds_sync();
+#pragma unroll
+        for (int st = K / 2; st > 0; st >>= 1) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                if ((i & st) == 0) {
+                    const int i2 = i + st;
+                    if (better(ms[i2], mi[i2], ms[i], mi[i])) {
+                        const float ts = ms[i];
+                        const uint32_t ti = mi[i];
+                        ms[i] = ms[i2];
+                        mi[i] = mi[i2];
+                        ms[i2] = ts;
+                        mi[i2] = ti;
+                    }
+                }
+            }
+        }
+        const int64_t q = qb + j * 32 + col;
+        if (half == 0 && qok[j]) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                if (i < k) {
+                    const bool ok = mi[i] != kEmptyId;
+                    os[q * k + i] = ok ? ms[i] : -FLT_MAX;
+                    oi[q * k + i] = ok ? static_cast<int64_t>(mi[i]) + a.id_offset : -1;
+                }
+            }
+        }
     }
 }
 
+template <typename T, int S, int K>
+int launch_cfg(const Args& a, const Plan& p, hipStream_t st) {
+    using C = Cfg<T, S, K>;
+    dim3 grid(static_cast<unsigned>((a.nq + C::QT - 1) / C::QT), static_cast<unsigned>(p.splits));
+    hipLaunchKernelGGL((flatip_topk_kernel<T, S, K>), grid, dim3(256), 0, st, a, p.items_per_split);
+    return check_launch("flatip_topk_kernel");
+}
+
+}  // namespace topk
+}  // namespace rt
+
+#include "topk_v1.h"
+
+namespace rt {
+namespace topk {
+
+// kernel choice: register lists (this file) for fp32 with k <= 32, the
+// candidate-buffer kernel (topk_v1.h) otherwise. Returns K, or 0 for v1.
+inline int list_k(bool f32, int k) { return (f32 && k <= 16) ? 16 : (f32 && k <= 32) ? 32 : 0; }
+
 template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
-    dim3 grid(static_cast<unsigned>((a.nq + kQT - 1) / kQT), static_cast<unsigned>(p.splits));
-    hipLaunchKernelGGL((flatip_topk_kernel<T, S>), grid, dim3(256), 0, st, a, p.cap, p.items_per_split);
-    return check_launch("flatip_topk_kernel");
+    constexpr bool F32 = sizeof(T) == 4;
+    if constexpr (F32) {
+        switch (list_k(true, a.k)) {
+            case 16: return launch_cfg<T, S, 16>(a, p, st);
+            case 32: return launch_cfg<T, S, 32>(a, p, st);
+            default: break;
+        }
+    }
+    return v1::launch_S<T, S>(a, p.cap, p.splits, p.items_per_split, st);
+}
+
+// compile-time shape facts the host planner needs, per (dtype, S)
+struct Shape {
+    int qt, nt, cap;
+};
+template <typename T, int S>
+Shape shape_S(int k) {
+    switch (list_k(sizeof(T) == 4, k)) {
+        case 16: return {Cfg<T, S, 16>::QT, Cfg<T, S, 16>::NT, 0};
+        case 32: return {Cfg<T, S, 32>::QT, Cfg<T, S, 32>::NT, 0};
+        default: return {v1::kQT, v1::kNT, v1::cap_for(k)};
+    }
 }
 
 // per-dtype entry points (defined in topk_{f32,f16,bf16}.hip)
 int launch_f32(const Args& a, const Plan& p, hipStream_t st);
 int launch_f16(const Args& a, const Plan& p, hipStream_t st);
 int launch_bf16(const Args& a, const Plan& p, hipStream_t st);
+Shape shape_f32(int d, int k);
+Shape shape_f16(int d, int k);
+Shape shape_bf16(int d, int k);
 
 }  // namespace topk
 }  // namespace rt
