@@ -174,6 +174,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the captured step")
     args = ap.parse_args()
 
     dist, rank, world, dev = dist_setup(args.gpus)
@@ -195,26 +196,45 @@ def main():
 
     for i in range(args.warmup):
         run(i)
-    # calibration step (untimed): which ABI call dominates the step?
+    # calibration step (eager, untimed): which ABI call dominates the step?
     TIMER.enable()
     run(args.warmup)
     cal = TIMER.summary()
     TIMER.disable()
     dominant = max(cal, key=lambda k: cal[k]["total_ms"])
 
+    # timed region: eager steps, HIP events around every launch of the dominant
+    # kernel on its launching stream (the roofline is measured live here).
+    # --graph replays the whole step as a captured hipGraph instead (roofline then
+    # from an eager pass right after).
+    if args.graph:
+        st_ids = tuple(t.clone() for t in batches[0])
+        step.capture(ut, mt, mt, user_ids=st_ids[0], pos_ids=st_ids[1], neg_ids=st_ids[2], warmup=1)
+
+        def run_timed(i):
+            for dst, src in zip(st_ids, batches[i % n_batches]):
+                dst.copy_(src, non_blocking=True)
+            return step.replay()
+    else:
+        run_timed = run
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
-    TIMER.enable([dominant])
+    if not args.graph:
+        TIMER.enable([dominant])
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss = run(i)
+        loss = run_timed(i)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if args.graph:
+        TIMER.enable([dominant])
+        for i in range(args.steps):
+            run(i)
     live = TIMER.summary()
     TIMER.disable()
     if dist is not None:
@@ -238,6 +258,8 @@ def main():
         roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None}
     roof.update({"kernel": dominant, "launches_per_step": d["count"] / args.steps,
+                 "measured": ("HIP events around each launch over an eager replay of the timed steps"
+                              if args.graph else "HIP events around each launch inside the timed region"),
                  "avg_launch_ms": d["avg_ms"], "step_share": cal[dominant]["total_ms"] /
                  max(1e-9, sum(v["total_ms"] for v in cal.values())),
                  "calibration_ms": {k: round(v["total_ms"], 4) for k, v in cal.items()}})

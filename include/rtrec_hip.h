@@ -166,6 +166,13 @@ typedef struct {
     float* l2_out;           /* [m, n] normalized rows (final layer) or NULL          */
     float* norms_out;        /* [m] row norms (with l2_out)                            */
     int64_t* num_batches_tracked; /* prev BN counter, +1 by block 0 in mode 1 (may be NULL) */
+    int64_t seg_split;       /* 0, or a multiple of 32 in (0, m): rows [0, seg_split) and
+                                [seg_split, m) are two SEPARATE BatchNorm batches (two tower
+                                calls — e.g. positives then negatives through the item
+                                tower — in one launch). Every per-column BN buffer above and
+                                below (prev_stats, save_mean/invstd, stats_out) is then
+                                [2][...] (segment-major), running stats are updated segment 0
+                                then segment 1, num_batches_tracked += 2. */
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
@@ -215,6 +222,8 @@ typedef struct {
     float* g_prev;           /* [m, k] or NULL */
     double* g_prev_stats;    /* [RT_STAT_SLOTS][2k] accumulated, caller zeroes (NULL = skip) */
     float* dsrc;             /* [m, k] input grad (first layer), or NULL */
+    int64_t seg_split;       /* as in rt_linear_fwd_args: g_stats, save_mean/invstd,
+                                prev_mean/invstd and g_prev_stats are then [2][...] */
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);

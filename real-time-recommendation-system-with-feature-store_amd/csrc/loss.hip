@@ -7,14 +7,21 @@
 // and the trainer's mixing 0.7·explicit + 0.3·in-batch
 // (src/training/trainers/two_tower.py:111-137), forward AND backward.
 //
-// Launch 1 (one block per 32 users): explicit CE with its gradients, then the
-//   in-batch row log-sum-exp by streaming 32-row item tiles through MFMA with an
-//   online max/sum (S never stored).
-// Launch 2 (2 × B/32 blocks): S is recomputed tile by tile; row blocks
-//   accumulate dU = dS·P, column blocks dP = dSᵀ·U (dS = w/B·(softmax(S) − I)),
-//   each wave owning a 32-wide slice of the tiles, reduced through LDS.
-// The k-order inside an MFMA chain is permuted (k = h·D/2 + s) so that every
-// fragment load is a contiguous 16-byte vector.
+// Block geometry of the in-batch part: a FIXED tile of 32 rows (users, or items
+// in the column pass) whose fragments sit in registers, and a STREAMED span of
+// 256 rows: each wave stages two 32-row tiles through its own LDS slice (all
+// loads of a tile in flight at once, the next tile prefetched into registers
+// while the current one is on the MFMAs).
+// Launch 1 (B/32 × B/256 blocks): per-span partial row log-sum-exp of S = U·Pᵀ/τ
+//   (online max/sum, S never stored), plus the explicit contrastive CE with its
+//   gradients for a strided subset of the block's users.
+// Launch 2 (2 × B/32 × B/256 blocks): S tiles are recomputed; the accumulator
+//   of an S tile is directly the A operand of the next MFMA (the k order over
+//   the streamed rows follows the accumulator layout), so dU = dS·P (row pass)
+//   and dP = dSᵀ·U (column pass) need no LDS transpose; dS = w/B·(softmax − I).
+//   The 4 waves' partials are summed through LDS, one atomic per element per span.
+// The k-order inside an S chain is permuted (k = h·D/2 + s) so that every
+// fragment is a contiguous 16-byte vector.
 #include <float.h>
 
 #include "rt_common.h"
@@ -34,43 +41,6 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// acc[r] = <A[a0 + tile_row(r,h)], Bm[b0 + (lane&31)]> (raw dot products)
-__device__ __forceinline__ f32x16 dot_tile(const float* __restrict__ A, int64_t a0, int64_t na,
-                                           const float* __restrict__ Bm, int64_t b0, int64_t nb, int D) {
-    const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-    int64_t ar = a0 + c, br = b0 + c;
-    ar = ar < na ? ar : na - 1;
-    br = br < nb ? br : nb - 1;
-    const float* pa = A + ar * D + h * (D / 2);
-    const float* pb = Bm + br * D + h * (D / 2);
-    f32x16 acc = {};
-    int s = 0;
-    for (; s + 16 <= D / 2; s += 16) {  // 8 independent 16-byte loads in flight
-        float4 av[4], bv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            av[j] = *reinterpret_cast<const float4*>(pa + s + 4 * j);
-            bv[j] = *reinterpret_cast<const float4*>(pb + s + 4 * j);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            acc = mfma(av[j].x, bv[j].x, acc);
-            acc = mfma(av[j].y, bv[j].y, acc);
-            acc = mfma(av[j].z, bv[j].z, acc);
-            acc = mfma(av[j].w, bv[j].w, acc);
-        }
-    }
-    for (; s < D / 2; s += 4) {
-        const float4 av = *reinterpret_cast<const float4*>(pa + s);
-        const float4 bv = *reinterpret_cast<const float4*>(pb + s);
-        acc = mfma(av.x, bv.x, acc);
-        acc = mfma(av.y, bv.y, acc);
-        acc = mfma(av.z, bv.z, acc);
-        acc = mfma(av.w, bv.w, acc);
-    }
-    return acc;
-}
-
 struct Args {
     const float* u; const float* p; const float* q;
     int64_t b; int d; int n_neg; float inv_tau;
@@ -80,17 +50,83 @@ struct Args {
     float* du; float* dp; float* dq; float* dub; float* dib;
     float2* part;       // workspace [n_split][b]: per-split (max, sum exp) of S rows
     float* diag;        // workspace [b]: S_ii = u_i·p_i / tau
-    int n_split;        // item splits of 128 (JT) per user tile
+    float* expl;        // workspace [b]: explicit CE term lse_i − pos_i
+    float* dposv;       // workspace [b]: d loss / d pos_i (= d loss / d bias share of user i)
+    int n_split;        // streamed spans of SPAN rows
+    int ib_blocks;      // launch-1 in-batch block rows (n_split, or 0 without the in-batch term)
     bool grad;
 };
 
-constexpr int JT = 128;  // streamed rows per block (4 waves x 32)
+constexpr int SPAN = 256;  // streamed rows per block (4 waves x 2 tiles of 32)
+constexpr int LDP = 4;     // LDS row pad (floats): conflict-free ds_read_b128 of 16 rows
+
+// ---- in-batch building blocks (DP = D padded to a multiple of 32) ----------
+// one wave loads 32 rows x DP floats of M (rows >= n and cols >= D read as 0)
+template <int DP>
+__device__ __forceinline__ void load_rows(const float* __restrict__ M, int64_t r0, int64_t n, int D,
+                                          float4 (&v)[DP / 8]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < DP / 8; ++u) {
+        const int e = lane + 64 * u;
+        const int row = e / (DP / 4), c = (e % (DP / 4)) * 4;
+        const int64_t gr = r0 + row;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gr < n && c < D) v[u] = *reinterpret_cast<const float4*>(M + gr * D + c);
+    }
+}
+template <int DP>
+__device__ __forceinline__ void store_rows(float* __restrict__ S, const float4 (&v)[DP / 8]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < DP / 8; ++u) {
+        const int e = lane + 64 * u;
+        const int row = e / (DP / 4), c = (e % (DP / 4)) * 4;
+        *reinterpret_cast<float4*>(S + row * (DP + LDP) + c) = v[u];
+    }
+}
+// fixed-row fragments: lane (c, h) holds F[f0 + c][h·DP/2 + s], s < DP/2
+template <int DP>
+__device__ __forceinline__ void load_fixed(const float* __restrict__ F, int64_t f0, int64_t n, int D,
+                                           float (&fx)[DP / 2]) {
+    const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+    const int64_t r = f0 + c;
+#pragma unroll
+    for (int q = 0; q < DP / 8; ++q) {
+        const int k = h * (DP / 2) + 4 * q;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (r < n && k < D) v = *reinterpret_cast<const float4*>(F + r * D + k);
+        fx[4 * q] = v.x; fx[4 * q + 1] = v.y; fx[4 * q + 2] = v.z; fx[4 * q + 3] = v.w;
+    }
+}
+// acc[r] = <streamed row tile_row(r,h) of Ss, fixed row (lane & 31)> (raw dots)
+template <int DP>
+__device__ __forceinline__ f32x16 s_tile(const float* __restrict__ Ss, const float (&fx)[DP / 2]) {
+    const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
+    const float* ap = Ss + c * (DP + LDP) + h * (DP / 2);
+    f32x16 acc = {};
+#pragma unroll
+    for (int q = 0; q < DP / 8; ++q) {
+        const float4 av = *reinterpret_cast<const float4*>(ap + 4 * q);
+        acc = mfma(av.x, fx[4 * q], acc);
+        acc = mfma(av.y, fx[4 * q + 1], acc);
+        acc = mfma(av.z, fx[4 * q + 2], acc);
+        acc = mfma(av.w, fx[4 * q + 3], acc);
+    }
+    return acc;
+}
+// dynamic LDS of the in-batch kernels: 4 waves x 32 rows x (DP + LDP) floats
+template <int DP>
+constexpr size_t inb_lds_bytes() { return static_cast<size_t>(4) * 32 * (DP + LDP) * sizeof(float); }
 
 // ---------------------------------------------------------------- launch 1
-// block (it, js): in-batch partial row log-sum-exp of users [32it, 32it+32) over
-// items [128js, 128js+128) (one 32x32 S^T tile per wave), plus the explicit
-// contrastive CE of a strided subset of the tile's users (one wave per user).
+// block (it, js < n_split): in-batch partial row log-sum-exp of users
+// [32it, 32it+32) over items [256js, 256js+256);
+// block (it, n_split + e), e < 8: explicit contrastive CE (+ gradients) of users
+// 32it + 4e + w, one wave per user, the negative rows loaded once.
+template <int DP>
 __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
+    extern __shared__ __attribute__((aligned(16))) float sm_f[];
     __shared__ float negs[4][kMaxNeg];
     __shared__ float red_m[4][RB], red_l[4][RB];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
@@ -100,156 +136,154 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
     const float bias = (a.ub ? a.ub[0] : 0.f) + (a.ib ? a.ib[0] : 0.f);
     const float inv_b = 1.f / static_cast<float>(a.b);
 
-    // ---- in-batch partial lse: S^T tile (items j × users i) ----
-    {
-        const int64_t t = static_cast<int64_t>(js) * 4 + w;   // item tile of this wave
+    if (js < a.ib_blocks) {
+        // ---- in-batch partial lse: S^T tiles (items j × users i) ----
+        float* Ss = sm_f + w * 32 * (DP + LDP);
+        float fx[DP / 2];
+        load_fixed<DP>(a.u, i0, a.b, D, fx);
+        const int64_t t0 = static_cast<int64_t>(js) * SPAN + 32 * w, t1 = t0 + 128;
+        float4 buf[DP / 8];
+        load_rows<DP>(a.p, t0, a.b, D, buf);
         float om = -INFINITY, ol = 0.f;
-        if (t * 32 < a.b) {
-            const f32x16 acc = dot_tile(a.p, t * 32, a.b, a.u, i0, a.b, D);
+#pragma unroll 1
+        for (int q = 0; q < 2; ++q) {
+            const int64_t tt = q == 0 ? t0 : t1;
+            if (tt >= a.b) break;  // wave-uniform
+            store_rows<DP>(Ss, buf);
+            wave_lds_sync();
+            if (q == 0 && t1 < a.b) load_rows<DP>(a.p, t1, a.b, D, buf);  // prefetch
+            const f32x16 acc = s_tile<DP>(Ss, fx);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int64_t j = t * 32 + tile_row(r, h);
-                if (j < a.b) {
+                if (tt + tile_row(r, h) < a.b) {
                     const float sv = acc[r] * a.inv_tau;
                     if (sv > om) { ol = ol * expf(om - sv) + 1.f; om = sv; }
                     else ol += expf(sv - om);
                 }
             }
+            wave_lds_sync();
         }
         const float m2 = __shfl_xor(om, 32, 64), l2 = __shfl_xor(ol, 32, 64);
         const float mm = fmaxf(om, m2);
         ol = (mm == -INFINITY) ? 0.f : ol * expf(om - mm) + l2 * expf(m2 - mm);
         if (h == 0) { red_m[w][c] = mm; red_l[w][c] = ol; }
-    }
-    __syncthreads();
-    if (w == 0 && h == 0 && i0 + c < a.b) {
-        float mm = -INFINITY;
-        for (int x = 0; x < 4; ++x) mm = fmaxf(mm, red_m[x][c]);
-        float ll = 0.f;
-        if (mm != -INFINITY)
-            for (int x = 0; x < 4; ++x) ll += red_l[x][c] * expf(red_m[x][c] - mm);
-        a.part[static_cast<int64_t>(js) * a.b + i0 + c] = make_float2(mm, ll);
+        __syncthreads();
+        if (w == 0 && h == 0 && i0 + c < a.b) {
+            float m3 = -INFINITY;
+            for (int x = 0; x < 4; ++x) m3 = fmaxf(m3, red_m[x][c]);
+            float ll = 0.f;
+            if (m3 != -INFINITY)
+                for (int x = 0; x < 4; ++x) ll += red_l[x][c] * expf(red_m[x][c] - m3);
+            a.part[static_cast<int64_t>(js) * a.b + i0 + c] = make_float2(m3, ll);
+        }
+        return;
     }
 
-    // ---- explicit negatives: users ii = 4js + w, stepping 4*n_split ----
-    double loss_e = 0.0;
-    float dbias_acc = 0.f;
-    for (int ii = js * 4 + w; ii < RB; ii += 4 * a.n_split) {
-        const int64_t i = i0 + ii;
-        if (i >= a.b) break;
-        const float* ur = a.u + i * D;
-        const float* pr = a.p + i * D;
-        float uv[kMaxD / 64], pv[kMaxD / 64];
-        float part = 0.f;
+    // ---- explicit negatives: blocks js >= n_split, one user per wave ----
+    const int64_t i = i0 + 4 * (js - a.ib_blocks) + w;
+    if (i >= a.b) return;
+    const float* ur = a.u + i * D;
+    const float* pr = a.p + i * D;
+    constexpr int V = kMaxD / 64;
+    float uv[V], pv[V];
+    float part = 0.f;
 #pragma unroll
-        for (int t = 0; t < kMaxD / 64; ++t) {
-            const int dd = lane + 64 * t;
-            uv[t] = dd < D ? ur[dd] : 0.f;
-            pv[t] = dd < D ? pr[dd] : 0.f;
-            part += uv[t] * pv[t];
-        }
-        const float dup = wave_sum(part) * a.inv_tau;
-        if (lane == 0) a.diag[i] = dup;
-        if (a.n_neg <= 0) {
-            if (a.grad) {
+    for (int t = 0; t < V; ++t) {
+        const int dd = lane + 64 * t;
+        uv[t] = dd < D ? ur[dd] : 0.f;
+        pv[t] = dd < D ? pr[dd] : 0.f;
+        part += uv[t] * pv[t];
+    }
+    // the first NG negative rows stay in registers for the gradient pass
+    float qv[NG][V];
+    auto load_q = [&](int g0) {
 #pragma unroll
-                for (int t = 0; t < kMaxD / 64; ++t) {
-                    const int dd = lane + 64 * t;
-                    if (dd < D) { a.du[i * D + dd] = 0.f; a.dp[i * D + dd] = 0.f; }
-                }
-            }
-            continue;
-        }
-        const float pos = dup + bias;
-        // all negative dots of a group of 16 at once: independent loads, one
-        // butterfly reduction for the 16 partial sums
-        float mx = pos;
-        for (int g0 = 0; g0 < a.n_neg; g0 += NG) {
-            float part_j[NG];
+        for (int jj = 0; jj < NG; ++jj) {
+            const int j = g0 + jj;
+            const float* qr = a.q + (i * a.n_neg + (j < a.n_neg ? j : 0)) * D;
 #pragma unroll
-            for (int jj = 0; jj < NG; ++jj) {
-                part_j[jj] = 0.f;
-                const int j = g0 + jj;
-                if (j < a.n_neg) {
-                    const float* qr = a.q + (i * a.n_neg + j) * D;
-#pragma unroll
-                    for (int t = 0; t < kMaxD / 64; ++t) {
-                        const int dd = lane + 64 * t;
-                        if (dd < D) part_j[jj] += uv[t] * qr[dd];
-                    }
-                }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-                for (int jj = 0; jj < NG; ++jj) part_j[jj] += __shfl_xor(part_j[jj], o, 64);
-#pragma unroll
-            for (int jj = 0; jj < NG; ++jj) {
-                if (g0 + jj < a.n_neg) {
-                    const float nv = part_j[jj] * a.inv_tau;
-                    if (lane == 0) negs[w][g0 + jj] = nv;
-                    mx = fmaxf(mx, nv);
-                }
+            for (int t = 0; t < V; ++t) {
+                const int dd = lane + 64 * t;
+                qv[jj][t] = (j < a.n_neg && dd < D) ? qr[dd] : 0.f;
             }
         }
-        wave_lds_sync();
-        float se = expf(pos - mx);
-        for (int j = 0; j < a.n_neg; ++j) se += expf(negs[w][j] - mx);
-        const float lse = mx + logf(se);
-        if (lane == 0) loss_e += static_cast<double>(lse - pos);
+    };
+    if (a.n_neg > 0) load_q(0);  // in flight with the positive dot's reduction
+    const float dup = wave_sum(part) * a.inv_tau;
+    if (lane == 0) a.diag[i] = dup;
+    if (a.n_neg <= 0) {
         if (a.grad) {
-            const float dpos = a.we * inv_b * (expf(pos - lse) - 1.f);
-            if (lane == 0) dbias_acc += dpos;
-            float duv[kMaxD / 64];
 #pragma unroll
-            for (int t = 0; t < kMaxD / 64; ++t) duv[t] = dpos * pv[t];
-            for (int g0 = 0; g0 < a.n_neg; g0 += NG) {
-                float qv[NG][kMaxD / 64];
-#pragma unroll
-                for (int jj = 0; jj < NG; ++jj) {
-                    const int j = g0 + jj;
-                    const float* qr = a.q + (i * a.n_neg + (j < a.n_neg ? j : 0)) * D;
-#pragma unroll
-                    for (int t = 0; t < kMaxD / 64; ++t) {
-                        const int dd = lane + 64 * t;
-                        qv[jj][t] = (j < a.n_neg && dd < D) ? qr[dd] : 0.f;
-                    }
-                }
-#pragma unroll
-                for (int jj = 0; jj < NG; ++jj) {
-                    const int j = g0 + jj;
-                    if (j >= a.n_neg) break;
-                    const float dn = a.we * inv_b * expf(negs[w][j] - lse);
-                    float* dqr = a.dq + (i * a.n_neg + j) * D;
-#pragma unroll
-                    for (int t = 0; t < kMaxD / 64; ++t) {
-                        const int dd = lane + 64 * t;
-                        if (dd < D) {
-                            duv[t] += dn * qv[jj][t];
-                            dqr[dd] = dn * uv[t] * a.inv_tau;
-                        }
-                    }
-                }
+            for (int t = 0; t < V; ++t) {
+                const int dd = lane + 64 * t;
+                if (dd < D) { a.du[i * D + dd] = 0.f; a.dp[i * D + dd] = 0.f; }
             }
+        }
+        return;
+    }
+    const float pos = dup + bias;
+    float mx = pos;
+    for (int g0 = 0; g0 < a.n_neg; g0 += NG) {
+        if (g0 > 0) load_q(g0);
+        float part_j[NG];
 #pragma unroll
-            for (int t = 0; t < kMaxD / 64; ++t) {
+        for (int jj = 0; jj < NG; ++jj) {
+            part_j[jj] = 0.f;
+#pragma unroll
+            for (int t = 0; t < V; ++t) part_j[jj] += uv[t] * qv[jj][t];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int jj = 0; jj < NG; ++jj) part_j[jj] += __shfl_xor(part_j[jj], o, 64);
+#pragma unroll
+        for (int jj = 0; jj < NG; ++jj) {
+            if (g0 + jj < a.n_neg) {
+                const float nv = part_j[jj] * a.inv_tau;
+                if (lane == 0) negs[w][g0 + jj] = nv;
+                mx = fmaxf(mx, nv);
+            }
+        }
+    }
+    wave_lds_sync();
+    float se = expf(pos - mx);
+    for (int j = 0; j < a.n_neg; ++j) se += expf(negs[w][j] - mx);
+    const float lse = mx + logf(se);
+    // per-user terms; launch 2 reduces them (one atomic per 32 users)
+    const float dpos = a.we * inv_b * (expf(pos - lse) - 1.f);
+    if (lane == 0) {
+        a.expl[i] = lse - pos;
+        a.dposv[i] = dpos;
+    }
+    if (!a.grad) return;
+    float duv[V];
+#pragma unroll
+    for (int t = 0; t < V; ++t) duv[t] = dpos * pv[t];
+    for (int g0 = 0; g0 < a.n_neg; g0 += NG) {
+        if (a.n_neg > NG) load_q(g0);  // registers still hold group 0 when n_neg <= NG
+#pragma unroll
+        for (int jj = 0; jj < NG; ++jj) {
+            const int j = g0 + jj;
+            if (j >= a.n_neg) break;
+            const float dn = a.we * inv_b * expf(negs[w][j] - lse);
+            float* dqr = a.dq + (i * a.n_neg + j) * D;
+#pragma unroll
+            for (int t = 0; t < V; ++t) {
                 const int dd = lane + 64 * t;
                 if (dd < D) {
-                    a.du[i * D + dd] = duv[t] * a.inv_tau;
-                    a.dp[i * D + dd] = dpos * uv[t] * a.inv_tau;
+                    duv[t] += dn * qv[jj][t];
+                    dqr[dd] = dn * uv[t] * a.inv_tau;
                 }
             }
         }
-        wave_lds_sync();
     }
-    if (lane == 0 && loss_e != 0.0) {
-        const double le = loss_e / static_cast<double>(a.b);
-        atomicAdd(&a.loss[1], le);
-        atomicAdd(&a.loss[0], a.we * le);
-    }
-    if (lane == 0 && a.grad && a.n_neg > 0 && dbias_acc != 0.f) {
-        if (a.dub) atomicAdd(a.dub, dbias_acc);
-        if (a.dib) atomicAdd(a.dib, dbias_acc);
+#pragma unroll
+    for (int t = 0; t < V; ++t) {
+        const int dd = lane + 64 * t;
+        if (dd < D) {
+            a.du[i * D + dd] = duv[t] * a.inv_tau;
+            a.dp[i * D + dd] = dpos * uv[t] * a.inv_tau;
+        }
     }
 }
 
@@ -266,84 +300,115 @@ __device__ __forceinline__ float combine_lse(const float2* part, int n_split, in
 }
 
 // ---------------------------------------------------------------- launch 2
-// blockIdx.z = 0: row pass, fixed 32 users, dU += dS · P over 128 streamed items
-// blockIdx.z = 1: column pass, fixed 32 items, dP += dSᵀ · U over 128 streamed users
-// (dS = wb/B·(softmax(S) − I)); results added atomically (n_split adds per element).
-template <int DT>  // D/32 output tiles per wave accumulator
+// blockIdx.z = 0: row pass, fixed 32 users, dU += dS · P over the span's items
+// blockIdx.z = 1: column pass, fixed 32 items, dP += dSᵀ · U over the span's users
+// (dS = wb/B·(softmax(S) − I)); one atomic add per output element per span.
+template <int DP>
 __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, bool add_loss) {
-    __shared__ float Ds[4][32][33];
-    __shared__ float lse_s[JT];       // row pass: [0,32) fixed users; column pass: 128 streamed users
-    __shared__ float red[32 * (kMaxD + 1)];
+    constexpr int DT = DP / 32;
+    extern __shared__ __attribute__((aligned(16))) float sm_b[];
+    __shared__ float lse_s[SPAN];  // column pass: the span's streamed users
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, c = lane & 31, h = lane >> 5;
     const int D = a.d;
     const bool row_pass = blockIdx.z == 0;
-    const int64_t f0 = static_cast<int64_t>(blockIdx.x) * RB;      // fixed tile
-    const int64_t s0 = static_cast<int64_t>(blockIdx.y) * JT;      // streamed range
-    const float* Str = row_pass ? a.p : a.u;
+    const int64_t f0 = static_cast<int64_t>(blockIdx.x) * RB;    // fixed tile
+    const int64_t s0 = static_cast<int64_t>(blockIdx.y) * SPAN;  // streamed span
+    const float* Fm = row_pass ? a.u : a.p;
+    const float* Sm = row_pass ? a.p : a.u;
     const float scale = wb_eff / static_cast<float>(a.b);
+    float lse_fixed = 0.f;  // row pass: lse of user f0 + c
+    const bool ib = wb_eff != 0.f;
     if (row_pass) {
-        if (tid < RB) {
-            const int64_t i = f0 + tid;
-            const float l = i < a.b ? combine_lse(a.part, a.n_split, a.b, i) : 0.f;
-            lse_s[tid] = l;
-            if (add_loss && blockIdx.y == 0 && i < a.b) {
-                const double li = static_cast<double>(l - a.diag[i]) / static_cast<double>(a.b);
-                atomicAdd(&a.loss[2], li);
-                atomicAdd(&a.loss[0], static_cast<double>(wb_eff) * li);
+        const int64_t i = f0 + c;
+        if (ib && i < a.b) lse_fixed = combine_lse(a.part, a.n_split, a.b, i);
+        if (add_loss && blockIdx.y == 0 && w == 0) {
+            // the loss scalars and bias grads of these 32 users: one atomic each
+            double li = 0.0, le = 0.0;
+            float dpb = 0.f;
+            if (h == 0 && i < a.b) {
+                if (ib) li = static_cast<double>(lse_fixed - a.diag[i]) / static_cast<double>(a.b);
+                if (a.n_neg > 0) {
+                    le = static_cast<double>(a.expl[i]) / static_cast<double>(a.b);
+                    dpb = a.dposv[i];
+                }
+            }
+            li = wave_sum(li);
+            le = wave_sum(le);
+            dpb = wave_sum(dpb);
+            if (lane == 0) {
+                if (ib) atomicAdd(&a.loss[2], li);
+                if (a.n_neg > 0) atomicAdd(&a.loss[1], le);
+                atomicAdd(&a.loss[0], static_cast<double>(wb_eff) * li + static_cast<double>(a.we) * le);
+                if (a.grad && a.n_neg > 0) {
+                    if (a.dub) atomicAdd(a.dub, dpb);
+                    if (a.dib) atomicAdd(a.dib, dpb);
+                }
             }
         }
-    } else if (tid < JT) {
+    } else {
         const int64_t i = s0 + tid;
         lse_s[tid] = i < a.b ? combine_lse(a.part, a.n_split, a.b, i) : 0.f;
     }
-    for (int e = tid; e < 32 * (kMaxD + 1); e += 256) red[e] = 0.f;
     __syncthreads();
-    if (!a.grad) return;
+    if (!a.grad || !ib) return;
+
+    float* Ss = sm_b + w * 32 * (DP + LDP);
+    float fx[DP / 2];
+    load_fixed<DP>(Fm, f0, a.b, D, fx);
+    const int64_t t0 = s0 + 32 * w, t1 = t0 + 128;
+    float4 buf[DP / 8];
+    load_rows<DP>(Sm, t0, a.b, D, buf);
     f32x16 acc[DT];
 #pragma unroll
     for (int x = 0; x < DT; ++x) acc[x] = f32x16{};
-    const int64_t t0 = s0 + w * 32;  // this wave's streamed tile
-    if (t0 < a.b) {
-        // row pass: (row = item j, col = user i);  column pass: (row = user i, col = item j)
-        const f32x16 st = row_pass ? dot_tile(a.p, t0, a.b, a.u, f0, a.b, D)
-                                   : dot_tile(a.u, t0, a.b, a.p, f0, a.b, D);
+#pragma unroll 1
+    for (int q = 0; q < 2; ++q) {
+        const int64_t tt = q == 0 ? t0 : t1;
+        if (tt >= a.b) break;  // wave-uniform
+        store_rows<DP>(Ss, buf);
+        wave_lds_sync();
+        if (q == 0 && t1 < a.b) load_rows<DP>(Sm, t1, a.b, D, buf);  // prefetch
+        // st[r]: streamed row tile_row(r,h) x fixed col c
+        const f32x16 st = s_tile<DP>(Ss, fx);
+        float ds[16];
+        const int64_t fcol = f0 + c;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int rr = tile_row(r, h);
-            const int64_t srow = t0 + rr;
-            const int64_t fcol = f0 + c;
-            float ds = 0.f;
+            const int64_t srow = tt + rr;
+            float v = 0.f;
             if (srow < a.b && fcol < a.b) {
-                const float lse = row_pass ? lse_s[c] : lse_s[w * 32 + rr];
-                const float pr = expf(st[r] * a.inv_tau - lse);
-                ds = scale * (pr - (srow == fcol ? 1.f : 0.f));
+                const float lse = row_pass ? lse_fixed : lse_s[32 * w + 128 * q + rr];
+                v = scale * (expf(st[r] * a.inv_tau - lse) - (srow == fcol ? 1.f : 0.f));
             }
-            Ds[w][c][rr] = ds;  // [fixed][streamed]
+            ds[r] = v;
         }
-        wave_lds_sync();
+        // dF[fixed c][d] += Σ_r dS[fixed c][streamed tile_row(r,h)] · Str[tile_row(r,h)][d]
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
-            const int dcol = dt * 32 + c;
-#pragma unroll 4
-            for (int s = 0; s < 16; ++s) {
-                const int ks = 2 * s + h;
-                const int64_t sr = t0 + ks;
-                const float bv = (sr < a.b && dcol < D) ? Str[sr * D + dcol] : 0.f;
-                acc[dt] = mfma(Ds[w][c][ks], bv, acc[dt]);
-            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                acc[dt] = mfma(ds[r], Ss[tile_row(r, h) * (DP + LDP) + dt * 32 + c], acc[dt]);
         }
+        wave_lds_sync();
     }
-    // reduce the 4 wave partials through LDS (red[fixed][d]), then atomically add
+    // ---- sum the 4 waves' [32 fixed x DP] partials through LDS, one atomic each ----
+    __syncthreads();  // every wave done with its Ss slice
+    float* red = sm_b;  // [4][DT*16][64]
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) atomicAdd(&red[tile_row(r, h) * (kMaxD + 1) + dt * 32 + c], acc[dt][r]);
+        for (int r = 0; r < 16; ++r) red[(w * DT * 16 + dt * 16 + r) * 64 + lane] = acc[dt][r];
     __syncthreads();
     float* out = row_pass ? a.du : a.dp;
-    for (int e = tid; e < 32 * D; e += 256) {
-        const int f = e / D, dd = e % D;
-        const int64_t gi = f0 + f;
-        if (gi < a.b) atomicAdd(&out[gi * D + dd], red[f * (kMaxD + 1) + dd] * a.inv_tau);
+    for (int p = tid; p < DT * 16 * 64; p += 256) {
+        const int v = p >> 6, l = p & 63;
+        const float t = red[v * 64 + l] + red[(DT * 16 + v) * 64 + l] + red[(2 * DT * 16 + v) * 64 + l] +
+                        red[(3 * DT * 16 + v) * 64 + l];
+        const int dt = v >> 4, r = v & 15;
+        const int64_t gi = f0 + tile_row(r, l >> 5);
+        const int dd = dt * 32 + (l & 31);
+        if (gi < a.b && dd < D) atomicAdd(&out[gi * D + dd], t * a.inv_tau);
     }
 }
 
@@ -370,6 +435,17 @@ __global__ __launch_bounds__(256) void similarity_kernel(const float* u, const f
 using namespace rt;
 
 namespace {
+// allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU); set once per kernel
+template <typename K>
+void allow_lds(K kernel, size_t bytes) {
+    static size_t set = 0;
+    if (bytes > set) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  static_cast<int>(bytes));
+        set = bytes;
+    }
+}
+
 int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, int d, int n_neg, float inv_tau,
              const float* ub, const float* ib, float we, float wb, double* loss_out, float* du, float* dp,
              float* dq, float* dub, float* dib, void* ws, size_t ws_bytes, void* stream, bool grad) {
@@ -378,34 +454,42 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
     if (d % 8 != 0 || d > loss::kMaxD || n_neg > loss::kMaxNeg) return RT_ERR_UNSUPPORTED;
     if (n_neg > 0 && !q) return RT_ERR_INVALID;
     if (grad && (!du || !dp || (n_neg > 0 && !dq))) return RT_ERR_INVALID;
-    const int n_split = static_cast<int>((b + loss::JT - 1) / loss::JT);
-    const size_t need = static_cast<size_t>(n_split) * b * sizeof(float2) + static_cast<size_t>(b) * sizeof(float);
+    const int n_split = static_cast<int>((b + loss::SPAN - 1) / loss::SPAN);
+    const size_t need = static_cast<size_t>(n_split) * b * sizeof(float2) + 3 * static_cast<size_t>(b) * sizeof(float);
     if (!ws || ws_bytes < need) return RT_ERR_WORKSPACE;
     if ((reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(p)) & 15) return RT_ERR_INVALID;
     float2* part = reinterpret_cast<float2*>(ws);
     float* diag = reinterpret_cast<float*>(part + static_cast<size_t>(n_split) * b);
     const float wb_eff = n_neg > 0 ? wb : 1.f;  // in-batch alone: the loss IS the in-batch CE (weight 1)
     const float we_eff = n_neg > 0 ? we : 0.f;
+    const bool want_ib = wb_eff != 0.f;
     loss::Args a{static_cast<const float*>(u), static_cast<const float*>(p), static_cast<const float*>(q),
                  b, d, n_neg, inv_tau, ub, ib, we_eff, wb_eff, loss_out, du, dp, dq, dub, dib, part, diag,
-                 n_split, grad};
+                 diag + b, diag + 2 * b, n_split, want_ib ? n_split : 0, grad};
     hipStream_t st = as_stream(stream);
     const unsigned nt = static_cast<unsigned>((b + loss::RB - 1) / loss::RB);
-    hipLaunchKernelGGL(loss::loss_fwd_kernel, dim3(nt, n_split), dim3(256), 0, st, a);
-    int rc = check_launch("loss_fwd_kernel");
-    if (rc) return rc;
-    const bool want_ib = wb_eff != 0.f;
-    if (!want_ib) return RT_OK;  // contrastive_loss alone
-    // forward-only calls still need launch 2's row pass for the in-batch loss value
-    const dim3 grid(nt, n_split, grad ? 2 : 1);
-    const int dt = (d + 31) / 32;
-    switch (dt) {
-        case 1: hipLaunchKernelGGL(loss::loss_bwd_kernel<1>, grid, dim3(256), 0, st, a, wb_eff, true); break;
-        case 2: hipLaunchKernelGGL(loss::loss_bwd_kernel<2>, grid, dim3(256), 0, st, a, wb_eff, true); break;
-        case 3:
-        case 4: hipLaunchKernelGGL(loss::loss_bwd_kernel<4>, grid, dim3(256), 0, st, a, wb_eff, true); break;
-        default: hipLaunchKernelGGL(loss::loss_bwd_kernel<8>, grid, dim3(256), 0, st, a, wb_eff, true); break;
+    const int dp32 = (d + 31) / 32 * 32;
+    // forward-only calls still need launch 2's row pass for the loss value
+    // launch 2 always runs: its row pass reduces the loss scalars and bias grads
+    const dim3 grid1(nt, a.ib_blocks + 8), grid2(nt, want_ib ? n_split : 1, (grad && want_ib) ? 2 : 1);
+#define RT_LOSS(DPV)                                                                                   \
+    do {                                                                                               \
+        const size_t lds = loss::inb_lds_bytes<DPV>();                                                 \
+        allow_lds(loss::loss_fwd_kernel<DPV>, lds);                                                    \
+        hipLaunchKernelGGL(loss::loss_fwd_kernel<DPV>, grid1, dim3(256), lds, st, a);                  \
+        int rc_ = check_launch("loss_fwd_kernel");                                                     \
+        if (rc_) return rc_;                                                                           \
+        allow_lds(loss::loss_bwd_kernel<DPV>, lds);                                                    \
+        hipLaunchKernelGGL(loss::loss_bwd_kernel<DPV>, grid2, dim3(256), lds, st, a, wb_eff, true);    \
+    } while (0)
+    switch (dp32) {
+        case 32: RT_LOSS(32); break;
+        case 64: RT_LOSS(64); break;
+        case 96:
+        case 128: RT_LOSS(128); break;
+        default: RT_LOSS(256); break;
     }
+#undef RT_LOSS
     return check_launch("loss_bwd_kernel");
 }
 }  // namespace
@@ -413,8 +497,8 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
 extern "C" size_t rt_twotower_loss_workspace_bytes(int64_t b, int d) {
     (void)d;
     if (b <= 0) return 256;
-    const int64_t n_split = (b + loss::JT - 1) / loss::JT;
-    return static_cast<size_t>(n_split) * b * sizeof(float2) + static_cast<size_t>(b) * sizeof(float) + 256;
+    const int64_t n_split = (b + loss::SPAN - 1) / loss::SPAN;
+    return static_cast<size_t>(n_split) * b * sizeof(float2) + 3 * static_cast<size_t>(b) * sizeof(float) + 256;
 }
 
 

@@ -82,35 +82,46 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
     const int64_t row0 = static_cast<int64_t>(blockIdx.x) * FM;
     const int64_t m = a.m;
 
+    // BatchNorm of the previous block: this block's batch is its row segment;
+    // block 0 derives every segment (it owns the save/running-stat writes,
+    // applied in segment order like two sequential tower calls)
+    const bool two = a.seg_split > 0;
+    const int my_seg = (two && row0 >= a.seg_split) ? 1 : 0;
     if (a.prev_mode == 1 || a.prev_mode == 2) {
+        const int nseg = two ? 2 : 1;
         for (int c = tid; c < k; c += 256) {
-            float mean, invstd, var_f = 0.f;
-            if (a.prev_mode == 1) {
-                double s1 = 0.0, s2 = 0.0;  // slot sums in slot order
+            for (int sg = 0; sg < nseg; ++sg) {
+                if (blockIdx.x != 0 && sg != my_seg) continue;
+                const int64_t ms = two ? (sg == 0 ? a.seg_split : m - a.seg_split) : m;
+                float mean, invstd, var_f = 0.f;
+                if (a.prev_mode == 1) {
+                    const double* ps = a.prev_stats + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * k;
+                    double s1 = 0.0, s2 = 0.0;  // slot sums in slot order
 #pragma unroll 4
-                for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
-                    s1 += a.prev_stats[static_cast<int64_t>(sl) * 2 * k + c];
-                    s2 += a.prev_stats[static_cast<int64_t>(sl) * 2 * k + k + c];
+                    for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                        s1 += ps[static_cast<int64_t>(sl) * 2 * k + c];
+                        s2 += ps[static_cast<int64_t>(sl) * 2 * k + k + c];
+                    }
+                    const double md = s1 / static_cast<double>(ms);
+                    double vd = s2 / static_cast<double>(ms) - md * md;
+                    vd = vd > 0.0 ? vd : 0.0;
+                    mean = static_cast<float>(md);
+                    invstd = static_cast<float>(1.0 / sqrt(vd + static_cast<double>(a.bn_eps)));
+                    var_f = static_cast<float>(ms > 1 ? vd * static_cast<double>(ms) / static_cast<double>(ms - 1) : vd);
+                } else {
+                    mean = a.running_mean[c];
+                    invstd = static_cast<float>(1.0 / sqrt(static_cast<double>(a.running_var[c]) + a.bn_eps));
                 }
-                const double md = s1 / static_cast<double>(m);
-                double vd = s2 / static_cast<double>(m) - md * md;
-                vd = vd > 0.0 ? vd : 0.0;
-                mean = static_cast<float>(md);
-                invstd = static_cast<float>(1.0 / sqrt(vd + static_cast<double>(a.bn_eps)));
-                var_f = static_cast<float>(m > 1 ? vd * static_cast<double>(m) / static_cast<double>(m - 1) : vd);
-            } else {
-                mean = a.running_mean[c];
-                invstd = static_cast<float>(1.0 / sqrt(static_cast<double>(a.running_var[c]) + a.bn_eps));
-            }
-            bn_affine(a.bn_gamma[c], a.bn_beta[c], mean, invstd, scale[c], shift[c]);
-            if (blockIdx.x == 0) {
-                if (c == 0 && a.prev_mode == 1 && a.num_batches_tracked) *a.num_batches_tracked += 1;
-                if (a.save_mean) a.save_mean[c] = mean;
-                if (a.save_invstd) a.save_invstd[c] = invstd;
-                if (a.prev_mode == 1 && a.running_mean) {
-                    const float mo = a.bn_momentum;
-                    a.running_mean[c] = (1.f - mo) * a.running_mean[c] + mo * mean;
-                    a.running_var[c] = (1.f - mo) * a.running_var[c] + mo * var_f;
+                if (sg == my_seg) bn_affine(a.bn_gamma[c], a.bn_beta[c], mean, invstd, scale[c], shift[c]);
+                if (blockIdx.x == 0) {
+                    if (c == 0 && a.prev_mode == 1 && a.num_batches_tracked) *a.num_batches_tracked += 1;
+                    if (a.save_mean) a.save_mean[sg * k + c] = mean;
+                    if (a.save_invstd) a.save_invstd[sg * k + c] = invstd;
+                    if (a.prev_mode == 1 && a.running_mean) {
+                        const float mo = a.bn_momentum;
+                        a.running_mean[c] = (1.f - mo) * a.running_mean[c] + mo * mean;
+                        a.running_var[c] = (1.f - mo) * a.running_var[c] + mo * var_f;
+                    }
                 }
             }
         }
@@ -225,7 +236,8 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
 
     // ---- epilogue ----
     const bool l2 = a.l2_out != nullptr;
-    double* const stats = a.stats_out ? a.stats_out + static_cast<int64_t>(blockIdx.x % RT_STAT_SLOTS) * 2 * n : nullptr;
+    double* const stats = a.stats_out ? a.stats_out + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
+                                                       blockIdx.x % RT_STAT_SLOTS) * 2 * n : nullptr;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
         const int ct = w + 4 * i;
@@ -298,6 +310,9 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
     float* Dz = sm;  // [FM][ldz]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
     const int64_t row0 = static_cast<int64_t>(blockIdx.x) * FM;
+    const bool two = a.seg_split > 0;
+    const int my_seg = (two && row0 >= a.seg_split) ? 1 : 0;
+    const int64_t seg_m = two ? (my_seg == 0 ? a.seg_split : m - a.seg_split) : m;
 
     // ---- phase A: dz tile ----
     if (a.grad_mode == 0) {
@@ -330,19 +345,20 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
         float* cC = cB + np;         // Σg·x̂/m
         float* cM = cC + np;         // mean
         float* cI = cM + np;         // invstd
-        const float inv_m = 1.f / static_cast<float>(m);
+        const float inv_m = 1.f / static_cast<float>(seg_m);
+        const double* gst = a.g_stats ? a.g_stats + static_cast<int64_t>(my_seg) * RT_STAT_SLOTS * 2 * n : nullptr;
         for (int c = tid; c < np; c += 256) {
             float A = 1.f, Bc = 0.f, C = 0.f, M = 0.f, I = 1.f;
             if (c < n && (a.grad_mode == 1 || a.grad_mode == 2)) {
-                I = a.save_invstd[c];
-                M = a.save_mean[c];
+                I = a.save_invstd[my_seg * n + c];
+                M = a.save_mean[my_seg * n + c];
                 A = a.bn_gamma[c] * I;
                 if (a.grad_mode == 1) {
                     double gs1 = 0.0, gs2 = 0.0;
 #pragma unroll 4
                     for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
-                        gs1 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + c];
-                        gs2 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + n + c];
+                        gs1 += gst[static_cast<int64_t>(sl) * 2 * n + c];
+                        gs2 += gst[static_cast<int64_t>(sl) * 2 * n + n + c];
                     }
                     Bc = static_cast<float>(gs1) * inv_m;
                     C = static_cast<float>(gs2) * inv_m;
@@ -409,14 +425,18 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
         }
     }
     if (blockIdx.x == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
+        // dgamma/dbeta of each BN batch (segment), summed like two tower calls' grads
         for (int c = tid; c < n; c += 256) {
-            double gs1 = 0.0, gs2 = 0.0;
-            for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
-                gs1 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + c];
-                gs2 += a.g_stats[static_cast<int64_t>(sl) * 2 * n + n + c];
+            for (int sg = 0; sg < (two ? 2 : 1); ++sg) {
+                const double* gs = a.g_stats + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * n;
+                double gs1 = 0.0, gs2 = 0.0;
+                for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                    gs1 += gs[static_cast<int64_t>(sl) * 2 * n + c];
+                    gs2 += gs[static_cast<int64_t>(sl) * 2 * n + n + c];
+                }
+                atomicAdd(&a.dgamma[c], static_cast<float>(gs2));  // atomic: concurrent chains of one tower
+                atomicAdd(&a.dbeta[c], static_cast<float>(gs1));
             }
-            atomicAdd(&a.dgamma[c], static_cast<float>(gs2));  // atomic: concurrent chains of one tower
-            atomicAdd(&a.dbeta[c], static_cast<float>(gs1));
         }
     }
     if (!a.g_prev && !a.dsrc) return;
@@ -458,14 +478,15 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
     const float pscale = a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f;
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
-    double* const gps = want_stats ? a.g_prev_stats + static_cast<int64_t>(blockIdx.x % RT_STAT_SLOTS) * 2 * k : nullptr;
+    double* const gps = want_stats ? a.g_prev_stats + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
+                                                        blockIdx.x % RT_STAT_SLOTS) * 2 * k : nullptr;
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
         const int kk = (w + 4 * i) * 32 + c32;
         const bool col_ok = kk < k;
         float s1 = 0.f, s2 = 0.f;
         float pmean = 0.f, pinv = 0.f;
-        if (want_stats && col_ok) { pmean = a.prev_mean[kk]; pinv = a.prev_invstd[kk]; }
+        if (want_stats && col_ok) { pmean = a.prev_mean[my_seg * k + kk]; pinv = a.prev_invstd[my_seg * k + kk]; }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t gr = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -546,16 +567,23 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a
 
     int gn[NT], gk[KT];
     bool n_ok[NT], k_ok[KT];
-    float sc[KT], sh[KT];
+    // BN affine of the previous block per column, per row segment (two BN batches)
+    float sc[2][KT], sh[2][KT];
+    const bool two = a.seg_split > 0;
 #pragma unroll
     for (int i = 0; i < NT; ++i) { gn[i] = n0 + 32 * i + c32; n_ok[i] = gn[i] < n; }
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
         gk[j] = k0 + 32 * j + c32;
         k_ok[j] = gk[j] < k;
-        sc[j] = 1.f; sh[j] = 0.f;
-        if ((a.prev_mode == 1 || a.prev_mode == 2) && k_ok[j])
-            bn_affine(a.prev_gamma[gk[j]], a.prev_beta[gk[j]], a.prev_mean[gk[j]], a.prev_invstd[gk[j]], sc[j], sh[j]);
+#pragma unroll
+        for (int sg = 0; sg < 2; ++sg) {
+            sc[sg][j] = 1.f; sh[sg][j] = 0.f;
+            const int so = two ? sg * k : 0;
+            if ((a.prev_mode == 1 || a.prev_mode == 2) && k_ok[j])
+                bn_affine(a.prev_gamma[gk[j]], a.prev_beta[gk[j]], a.prev_mean[so + gk[j]], a.prev_invstd[so + gk[j]],
+                          sc[sg][j], sh[sg][j]);
+        }
     }
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
@@ -592,7 +620,9 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a
             const int64_t r = g + 2 * u + h;
 #pragma unroll
             for (int j = 0; j < KT; ++j) {
-                const float xa = pro_col<PRO>(pro, slope, r, gk[j], sc[j], sh[j], x[u][j]);
+                const int sg = (two && r >= a.seg_split) ? 1 : 0;
+                const float xa = pro_col<PRO>(pro, slope, r, gk[j], sg ? sc[1][j] : sc[0][j], sg ? sh[1][j] : sh[0][j],
+                                              x[u][j]);
 #pragma unroll
                 for (int i = 0; i < NT; ++i) acc[i][j] = mfma(d[u][i], xa, acc[i][j]);
             }
@@ -680,6 +710,8 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
     if (a.m < 0 || a.k <= 0 || a.n <= 0 || !a.src || !a.w || a.ld_src < a.k) return RT_ERR_INVALID;
     if (a.n > 512 || a.k > 8192) return RT_ERR_UNSUPPORTED;
     if (a.prev_mode < 0 || a.prev_mode > 3) return RT_ERR_INVALID;
+    if (a.seg_split < 0 || (a.seg_split > 0 && (a.seg_split >= a.m || a.seg_split % mlp::FM != 0)))
+        return RT_ERR_INVALID;
     if (a.prev_mode == 1 && (!a.prev_stats || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.m == 0) return RT_OK;
@@ -717,6 +749,8 @@ static int validate_bwd(const rt_linear_bwd_args* args) {
     if ((a.grad_mode == 1 || a.grad_mode == 2) && (!a.g_stats || !a.save_mean || !a.save_invstd || !a.bn_gamma))
         return RT_ERR_INVALID;
     if (a.grad_mode < 0 || a.grad_mode > 3) return RT_ERR_INVALID;
+    if (a.seg_split < 0 || (a.seg_split > 0 && (a.seg_split >= a.m || a.seg_split % mlp::FM != 0)))
+        return RT_ERR_INVALID;
     if ((a.prev_mode == 1 || a.prev_mode == 2) &&
         (!a.prev_mean || !a.prev_invstd || !a.prev_gamma || !a.prev_beta))
         return RT_ERR_INVALID;

@@ -193,6 +193,7 @@ class ChainCtx:
     out: Optional[torch.Tensor] = None
     norms: Optional[torch.Tensor] = None
     normalize: bool = True
+    seg_split: int = 0  # > 0: rows [0, seg_split) and [seg_split, m) are separate BN batches
 
 
 def _stream(t: torch.Tensor):
@@ -202,16 +203,18 @@ def _stream(t: torch.Tensor):
 STAT_SLOTS = 16  # RT_STAT_SLOTS (include/rtrec_hip.h): BN sums are [slots][2][width] fp64
 
 
-def stats_arena_size(blocks: List[Block]) -> int:
+def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
     """fp64 words of BN column sums one forward (or backward) of the chain needs."""
-    return max(1, STAT_SLOTS * 2 * sum(b.linear.out_features for b in blocks[:-1]))
+    return max(1, n_seg * STAT_SLOTS * 2 * sum(b.linear.out_features for b in blocks[:-1]))
 
 
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
                   normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
-                  stats_arena: Optional[torch.Tensor] = None) -> ChainCtx:
+                  stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0) -> ChainCtx:
     """Run the block chain. ``src`` is the dense input [rows, k0] (fp32) or a
-    feature table when ``ids`` selects its rows (fused gather)."""
+    feature table when ``ids`` selects its rows (fused gather). ``seg_split`` > 0
+    runs two tower calls in one chain: rows [0, seg_split) and [seg_split, m)
+    are separate BatchNorm batches (running stats updated in that order)."""
     native.require_device(src, what="tower forward")
     if src.dtype != torch.float32:
         raise TypeError("tower input must be fp32 (the reference towers are fp32)")
@@ -226,18 +229,22 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         # what F.linear raises for the same mismatch
         raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({m}x{src.shape[-1]} and "
                            f"{k0}x{blocks[0].linear.out_features})")
+    n_seg = 2 if seg_split else 1
+    if seg_split and (seg_split % 32 != 0 or not 0 < seg_split < m):
+        raise ValueError("seg_split must be a multiple of 32 inside (0, m)")
+    seg_rows = [seg_split, m - seg_split] if seg_split else [m]
     for b in blocks[:-1]:
-        if b.bn is not None and b.bn.training and m <= 1:
+        if b.bn is not None and b.bn.training and min(seg_rows) <= 1:
             raise ValueError("Expected more than 1 value per channel when training (BatchNorm1d)")
-    ctx = ChainCtx(m=m, src=src, ids=ids, normalize=normalize)
+    ctx = ChainCtx(m=m, src=src, ids=ids, normalize=normalize, seg_split=seg_split)
     # one fp64 arena for all BN column sums of this call
     widths = [b.linear.out_features for b in blocks[:-1]]
     if stats_arena is None:  # caller-provided arenas are zeroed by the caller (one memset per step)
-        stats_arena = torch.zeros(stats_arena_size(blocks), dtype=torch.float64, device=dev)
+        stats_arena = torch.zeros(stats_arena_size(blocks, n_seg), dtype=torch.float64, device=dev)
     stats, off = [], 0
     for wdt in widths:
-        stats.append(stats_arena[off:off + STAT_SLOTS * 2 * wdt])
-        off += STAT_SLOTS * 2 * wdt
+        stats.append(stats_arena[off:off + n_seg * STAT_SLOTS * 2 * wdt])
+        off += n_seg * STAT_SLOTS * 2 * wdt
     st = _stream(src)
     cur_src, cur_ids, ld = src, ids, src.shape[1]
     for li, b in enumerate(blocks):
@@ -253,6 +260,7 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         a.w = lin.weight.data_ptr()
         a.bias = lin.bias.data_ptr() if lin.bias is not None else None
         a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
+        a.seg_split = seg_split
         if li == 0:
             a.prev_mode = 0
         else:
@@ -267,8 +275,8 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
                 a.bn_beta = pb.bn.bias.data_ptr()
                 a.running_mean = pb.bn.running_mean.data_ptr()
                 a.running_var = pb.bn.running_var.data_ptr()
-                sm = torch.empty(lin.in_features, dtype=torch.float32, device=dev)
-                si = torch.empty(lin.in_features, dtype=torch.float32, device=dev)
+                sm = torch.empty(n_seg * lin.in_features, dtype=torch.float32, device=dev)
+                si = torch.empty(n_seg * lin.in_features, dtype=torch.float32, device=dev)
                 ctx.save_mean[li - 1], ctx.save_invstd[li - 1] = sm, si
                 a.save_mean = sm.data_ptr()
                 a.save_invstd = si.data_ptr()
@@ -319,12 +327,13 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
     max_w = max(b.linear.out_features for b in blocks)
     dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev)
     widths = [b.linear.out_features for b in blocks[:-1]]
+    n_seg = 2 if ctx.seg_split else 1
     gst_arena = stats_arena if stats_arena is not None else \
-        torch.zeros(stats_arena_size(blocks), dtype=torch.float64, device=dev)
+        torch.zeros(stats_arena_size(blocks, n_seg), dtype=torch.float64, device=dev)
     gstats, off = [], 0
     for wdt in widths:
-        gstats.append(gst_arena[off:off + STAT_SLOTS * 2 * wdt])
-        off += STAT_SLOTS * 2 * wdt
+        gstats.append(gst_arena[off:off + n_seg * STAT_SLOTS * 2 * wdt])
+        off += n_seg * STAT_SLOTS * 2 * wdt
     gs: List[Optional[torch.Tensor]] = [None] * L
     dsrc = torch.empty((m, blocks[0].linear.in_features), dtype=torch.float32, device=dev) if want_dsrc else None
     for li in range(L, -1, -1):
@@ -337,6 +346,7 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         a.dbias = slab.grad_of(lin.bias).data_ptr() if lin.bias is not None else None
         a.dz_ws = dz_ws.data_ptr()
         a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
+        a.seg_split = ctx.seg_split
         if li == L:
             if ctx.normalize:
                 a.grad_mode = 0

@@ -49,7 +49,7 @@ class LinearFwdArgs(ctypes.Structure):
         ("running_mean", vp), ("running_var", vp), ("save_mean", vp), ("save_invstd", vp),
         ("bn_eps", c_f32), ("bn_momentum", c_f32), ("drop_p", c_f32), ("drop_seed", c_u64),
         ("seed_offset", vp), ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
-        ("num_batches_tracked", vp),
+        ("num_batches_tracked", vp), ("seg_split", c_i64),
     ]
 
 
@@ -62,7 +62,7 @@ class LinearBwdArgs(ctypes.Structure):
         ("src", vp), ("src_rows", c_i64), ("ld_src", c_int), ("ids", vp),
         ("prev_mode", c_int), ("prev_act", c_int), ("prev_mean", vp), ("prev_invstd", vp),
         ("prev_gamma", vp), ("prev_beta", vp), ("prev_drop_p", c_f32), ("prev_drop_seed", c_u64),
-        ("seed_offset", vp), ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp),
+        ("seed_offset", vp), ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp), ("seg_split", c_i64),
     ]
 
 

@@ -51,12 +51,17 @@ class FusedTrainStep:
             parts.append(self.arena[off:off + sz])
             off += sz
         (self.a_uf, self.a_pf, self.a_nf, self.a_ub, self.a_pb, self.a_nb, self.loss_buf, self.sumsq) = parts
+        # the pos and neg arenas are adjacent: together they are the [2]-segment
+        # arena of the merged item chain
+        self.a_pqf = self.arena[ua:ua + 2 * ia]
+        self.a_pqb = self.arena[2 * ua + 2 * ia:2 * ua + 4 * ia]
         self.lr, self.wd, self.max_norm = lr, weight_decay, max_norm
         self.b1, self.b2 = betas
         self.eps = eps
         self.we, self.wb = explicit_weight, in_batch_weight
         self.steps = 0
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.graph_update: Optional[torch.cuda.CUDAGraph] = None
         self.static: Dict[str, torch.Tensor] = {}
         # the user chain and the positive-item chain overlap the negative-item chain
         # (three independent towers calls; BN running stats of the item tower still
@@ -101,6 +106,12 @@ class FusedTrainStep:
 
     # ------------------------------------------------------------------
     def _run(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None):
+        self._grads(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
+        self._allreduce()
+        return self._update()
+
+    def _grads(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None):
+        """Forward, fused loss, backward: parameter grads in the slab."""
         m = self.model
         ub = blocks_from_sequential(m.user_tower.mlp)
         ib = blocks_from_sequential(m.item_tower.mlp)
@@ -114,39 +125,70 @@ class FusedTrainStep:
         s_u.wait_stream(main)
         with torch.cuda.stream(s_u):
             u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
-        p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf)
-        q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
-            if (neg_src is not None) else None
+        b = u.m
+        # positives and negatives go through the item tower as ONE chain of
+        # B + B·N rows whose two row segments are separate BatchNorm batches
+        # (the reference's two item-tower calls, src/training/trainers/two_tower.py:
+        # 107-121): half the item-tower launches. Needs B % 32 == 0.
+        merged = neg_src is not None and b % 32 == 0 and (
+            (pos_ids is not None and neg_ids is not None and pos_src is neg_src) or
+            (pos_ids is None and neg_ids is None))
+        if merged:
+            if pos_ids is not None:
+                item_src, item_ids = pos_src, torch.cat([pos_ids.reshape(-1), neg_ids.reshape(-1)])
+            else:
+                item_src, item_ids = torch.cat([pos_src, neg_src]), None
+            pq = chain_forward(ib, item_src, item_ids, seed_offset=so, stats_arena=self.a_pqf, seg_split=b)
+            p_out, q_out = pq.out[:b], pq.out[b:]
+        else:
+            p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf)
+            q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
+                if (neg_src is not None) else None
+            p_out, q_out = p.out, (q.out if q is not None else None)
         main.wait_stream(s_u)
-        b, d = u.out.shape
-        n_neg = (q.m // b) if q is not None else 0
+        d = u.out.shape[1]
+        n_neg = (q_out.shape[0] // b) if q_out is not None else 0
         du = torch.empty_like(u.out)
-        dp = torch.empty_like(p.out)
-        dq = torch.empty_like(q.out) if q is not None else None
+        if merged:
+            dpq = torch.empty_like(pq.out)
+            dp, dq = dpq[:b], dpq[b:]
+        else:
+            dp = torch.empty_like(p_out)
+            dq = torch.empty_like(q_out) if q_out is not None else None
         ws = kernels.workspace(self.dev, native.lib().rt_twotower_loss_workspace_bytes(b, d), "loss")
         ubias, ibias = m.user_bias, m.item_bias
         with TIMER.region("loss_fwd_bwd", flops=6.0 * b * b * d + 6.0 * b * (n_neg + 1) * d,
                           bytes_=4.0 * d * (4 * b + 2 * b * n_neg)):
-            call("rt_twotower_loss_fwd_bwd", ptr(u.out), ptr(p.out), ptr(q.out) if q is not None else None, 0, b,
-                 d, n_neg, 1.0 / m.temperature, ptr(ubias), ptr(ibias), self.we, self.wb, ptr(self.loss_buf),
+            call("rt_twotower_loss_fwd_bwd", ptr(u.out), ptr(p_out), ptr(q_out) if q_out is not None else None, 0,
+                 b, d, n_neg, 1.0 / m.temperature, ptr(ubias), ptr(ibias), self.we, self.wb, ptr(self.loss_buf),
                  ptr(du), ptr(dp), ptr(dq),
                  ptr(slab.grad_of(ubias)) if ubias is not None else None,
                  ptr(slab.grad_of(ibias)) if ibias is not None else None, ptr(ws), ws.numel(), st)
-        # backward: three independent chains (grads meet in the slab through atomics)
+        # backward: independent chains (grads meet in the slab through atomics)
         s_u.wait_stream(main)
-        s_p.wait_stream(main)
         with torch.cuda.stream(s_u):
             chain_backward(ub, u, du, slab, seed_offset=so, stats_arena=self.a_ub, attach=False)
-        with torch.cuda.stream(s_p):
-            chain_backward(ib, p, dp, slab, seed_offset=so, stats_arena=self.a_pb, attach=False)
-        if q is not None:
-            chain_backward(ib, q, dq, slab, seed_offset=so, stats_arena=self.a_nb, attach=False)
+        if merged:
+            chain_backward(ib, pq, dpq, slab, seed_offset=so, stats_arena=self.a_pqb, attach=False)
+        else:
+            s_p.wait_stream(main)
+            with torch.cuda.stream(s_p):
+                chain_backward(ib, p, dp, slab, seed_offset=so, stats_arena=self.a_pb, attach=False)
+            if q is not None:
+                chain_backward(ib, q, dq, slab, seed_offset=so, stats_arena=self.a_nb, attach=False)
+            main.wait_stream(s_p)
         main.wait_stream(s_u)
-        main.wait_stream(s_p)
+
+    def _allreduce(self):
         if self.pg is not None:  # data parallel: average the flat grad slab (one RCCL all-reduce)
             import torch.distributed as dist
-            dist.all_reduce(slab.grad, op=dist.ReduceOp.SUM, group=self.pg)
-            slab.grad.mul_(1.0 / dist.get_world_size(self.pg))
+            dist.all_reduce(self.slab.grad, op=dist.ReduceOp.SUM, group=self.pg)
+            self.slab.grad.mul_(1.0 / dist.get_world_size(self.pg))
+
+    def _update(self):
+        """clip_grad_norm_ + Adam on the flat slabs (device step counter / lr)."""
+        slab = self.slab
+        st = native.stream_of(slab.data)
         nb = slab.data.numel() * 4.0
         with TIMER.region("clip_adam", flops=0.0, bytes_=nb * 7):
             call("rt_grad_sqnorm", ptr(slab.grad), ptr(slab.tensor_offsets()), len(slab.params), ptr(self.sumsq),
@@ -171,6 +213,10 @@ class FusedTrainStep:
     # ------------------------------------------------------------------
     # hipGraph capture of the whole step (ids/features in static buffers)
     def capture(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None, warmup: int = 2):
+        """Capture the step as hipGraph(s) over static inputs (copy new ids /
+        features into the tensors passed here, then ``replay()``). With a
+        process group the step is two graphs — gradients, then clip+Adam — with
+        the RCCL all-reduce launched eagerly between them."""
         self.model.train()
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
@@ -180,13 +226,24 @@ class FusedTrainStep:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._run(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
+            self._grads(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
+            if self.pg is None:
+                self._update()
         self.graph = g
-        self.steps += warmup + 1
+        self.graph_update = None
+        if self.pg is not None:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._update()
+            self.graph_update = g2
+        self.steps += warmup
         return g
 
     def replay(self):
         self.graph.replay()
+        if self.graph_update is not None:
+            self._allreduce()
+            self.graph_update.replay()
         self.steps += 1
         return self.loss_buf
 
