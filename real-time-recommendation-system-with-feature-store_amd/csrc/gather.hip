@@ -13,6 +13,10 @@ namespace gather {
 
 constexpr int kUnroll = 4;
 
+// element vectors as clang ext_vector types (the nontemporal builtins need them)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
 // IDX: uint32_t when n_ids * vecs_per_row < 2^32 (cheap division), else int64_t
 template <typename V, typename IDX>
 __global__ __launch_bounds__(256) void gather_rows_kernel(const V* __restrict__ table, int64_t row_begin,
@@ -36,7 +40,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const V* __restrict__ 
                 const uint32_t c = static_cast<uint32_t>(e - r * vecs_per_row);
                 const int64_t id = ids[r] - row_begin;
                 if (id >= 0 && id < n_rows) {
-                    v[u] = table[id * vecs_per_row + c];
+                    v[u] = __builtin_nontemporal_load(table + id * vecs_per_row + c);  // read once
                 } else {
                     v[u] = V{};
                     if (c == 0 && oob) atomicAdd(oob, 1);
@@ -45,7 +49,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const V* __restrict__ 
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u)
-            if (has[u]) out[dst[u]] = v[u];
+            if (has[u]) __builtin_nontemporal_store(v[u], out + dst[u]);  // streamed out, not re-read here
     }
 }
 
@@ -94,9 +98,9 @@ __global__ __launch_bounds__(64) void l2_renorm_kernel(float* __restrict__ x, in
     }
 }
 
-inline unsigned grid_for(int64_t work, int block) {
+inline unsigned grid_for(int64_t work, int block, int64_t cap = 4096) {
     int64_t g = (work + block - 1) / block;
-    if (g > 4096) g = 4096;  // 256 CUs x 16 blocks; grid-stride the rest
+    if (g > cap) g = cap;  // grid-stride the rest
     if (g < 1) g = 1;
     return static_cast<unsigned>(g);
 }
@@ -109,7 +113,9 @@ using namespace rt;
 template <typename V>
 static void launch_gather(const void* table, int64_t row_begin, int64_t n_rows, uint32_t vpr, const int64_t* ids,
                           int64_t n_ids, void* out, int32_t* oob, hipStream_t st) {
-    const unsigned grid = gather::grid_for(n_ids * vpr / gather::kUnroll, 256);
+    // large grids keep more independent row reads in flight across the chip
+    // (probe: 4096 -> 65536 blocks raised a float4 copy from 4.6 to 5.3 TB/s)
+    const unsigned grid = gather::grid_for(n_ids * vpr / gather::kUnroll, 256, 65536);
     if (n_ids * static_cast<int64_t>(vpr) + static_cast<int64_t>(grid) * 256 * gather::kUnroll < (1ll << 32)) {
         hipLaunchKernelGGL((gather::gather_rows_kernel<V, uint32_t>), dim3(grid), dim3(256), 0, st,
                            reinterpret_cast<const V*>(table), row_begin, n_rows, vpr, ids, n_ids,
@@ -130,10 +136,10 @@ extern "C" int rt_gather_rows(const void* table, int64_t row_begin, int64_t n_ro
     hipStream_t st = as_stream(stream);
     const uintptr_t al = reinterpret_cast<uintptr_t>(table) | reinterpret_cast<uintptr_t>(out);
     if ((row_bytes & 15) == 0 && (al & 15) == 0) {
-        launch_gather<uint4>(table, row_begin, n_rows, static_cast<uint32_t>(row_bytes / 16), ids, n_ids, out,
+        launch_gather<gather::u32x4>(table, row_begin, n_rows, static_cast<uint32_t>(row_bytes / 16), ids, n_ids, out,
                              oob_count, st);
     } else if ((row_bytes & 7) == 0 && (al & 7) == 0) {
-        launch_gather<uint2>(table, row_begin, n_rows, static_cast<uint32_t>(row_bytes / 8), ids, n_ids, out,
+        launch_gather<gather::u32x2>(table, row_begin, n_rows, static_cast<uint32_t>(row_bytes / 8), ids, n_ids, out,
                              oob_count, st);
     } else {
         if (al & 3) return RT_ERR_INVALID;
