@@ -42,7 +42,7 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 struct Args {
-    const float* u; const float* p; const float* q;
+    const void* u; const void* p; const void* q;  // element type = the kernel's T
     int64_t b; int d; int n_neg; float inv_tau;
     const float* ub; const float* ib;
     float we, wb;       // weights of the explicit / in-batch terms in loss_out[0]
@@ -62,8 +62,20 @@ constexpr int LDP = 4;     // LDS row pad (floats): conflict-free ds_read_b128 o
 
 // ---- in-batch building blocks (DP = D padded to a multiple of 32) ----------
 // one wave loads 32 rows x DP floats of M (rows >= n and cols >= D read as 0)
-template <int DP>
-__device__ __forceinline__ void load_rows(const float* __restrict__ M, int64_t r0, int64_t n, int D,
+// 4 consecutive elements widened to fp32 (16-bit types: one 8-byte load)
+template <typename T>
+__device__ __forceinline__ float4 load4(const T* __restrict__ p) {
+    if constexpr (sizeof(T) == 4) {
+        return *reinterpret_cast<const float4*>(p);
+    } else {
+        const uint2 r = *reinterpret_cast<const uint2*>(p);
+        const T* e = reinterpret_cast<const T*>(&r);
+        return make_float4(to_f32(e[0]), to_f32(e[1]), to_f32(e[2]), to_f32(e[3]));
+    }
+}
+
+template <int DP, typename T>
+__device__ __forceinline__ void load_rows(const T* __restrict__ M, int64_t r0, int64_t n, int D,
                                           float4 (&v)[DP / 8]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -72,7 +84,7 @@ __device__ __forceinline__ void load_rows(const float* __restrict__ M, int64_t r
         const int row = e / (DP / 4), c = (e % (DP / 4)) * 4;
         const int64_t gr = r0 + row;
         v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gr < n && c < D) v[u] = *reinterpret_cast<const float4*>(M + gr * D + c);
+        if (gr < n && c < D) v[u] = load4<T>(M + gr * D + c);
     }
 }
 template <int DP>
@@ -86,8 +98,8 @@ __device__ __forceinline__ void store_rows(float* __restrict__ S, const float4 (
     }
 }
 // fixed-row fragments: lane (c, h) holds F[f0 + c][h·DP/2 + s], s < DP/2
-template <int DP>
-__device__ __forceinline__ void load_fixed(const float* __restrict__ F, int64_t f0, int64_t n, int D,
+template <int DP, typename T>
+__device__ __forceinline__ void load_fixed(const T* __restrict__ F, int64_t f0, int64_t n, int D,
                                            float (&fx)[DP / 2]) {
     const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
     const int64_t r = f0 + c;
@@ -95,7 +107,7 @@ __device__ __forceinline__ void load_fixed(const float* __restrict__ F, int64_t 
     for (int q = 0; q < DP / 8; ++q) {
         const int k = h * (DP / 2) + 4 * q;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < n && k < D) v = *reinterpret_cast<const float4*>(F + r * D + k);
+        if (r < n && k < D) v = load4<T>(F + r * D + k);
         fx[4 * q] = v.x; fx[4 * q + 1] = v.y; fx[4 * q + 2] = v.z; fx[4 * q + 3] = v.w;
     }
 }
@@ -124,8 +136,11 @@ constexpr size_t inb_lds_bytes() { return static_cast<size_t>(4) * 32 * (DP + LD
 // [32it, 32it+32) over items [256js, 256js+256);
 // block (it, n_split + e), e < 8: explicit contrastive CE (+ gradients) of users
 // 32it + 4e + w, one wave per user, the negative rows loaded once.
-template <int DP>
+template <int DP, typename T>
 __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
+    const T* __restrict__ U = static_cast<const T*>(a.u);
+    const T* __restrict__ P = static_cast<const T*>(a.p);
+    const T* __restrict__ Qn = static_cast<const T*>(a.q);
     extern __shared__ __attribute__((aligned(16))) float sm_f[];
     __shared__ float negs[4][kMaxNeg];
     __shared__ float red_m[4][RB], red_l[4][RB];
@@ -140,10 +155,10 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
         // ---- in-batch partial lse: S^T tiles (items j × users i) ----
         float* Ss = sm_f + w * 32 * (DP + LDP);
         float fx[DP / 2];
-        load_fixed<DP>(a.u, i0, a.b, D, fx);
+        load_fixed<DP, T>(U, i0, a.b, D, fx);
         const int64_t t0 = static_cast<int64_t>(js) * SPAN + 32 * w, t1 = t0 + 128;
         float4 buf[DP / 8];
-        load_rows<DP>(a.p, t0, a.b, D, buf);
+        load_rows<DP, T>(P, t0, a.b, D, buf);
         float om = -INFINITY, ol = 0.f;
 #pragma unroll 1
         for (int q = 0; q < 2; ++q) {
@@ -151,7 +166,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
             if (tt >= a.b) break;  // wave-uniform
             store_rows<DP>(Ss, buf);
             wave_lds_sync();
-            if (q == 0 && t1 < a.b) load_rows<DP>(a.p, t1, a.b, D, buf);  // prefetch
+            if (q == 0 && t1 < a.b) load_rows<DP, T>(P, t1, a.b, D, buf);  // prefetch
             const f32x16 acc = s_tile<DP>(Ss, fx);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -182,16 +197,16 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
     // ---- explicit negatives: blocks js >= n_split, one user per wave ----
     const int64_t i = i0 + 4 * (js - a.ib_blocks) + w;
     if (i >= a.b) return;
-    const float* ur = a.u + i * D;
-    const float* pr = a.p + i * D;
+    const T* ur = U + i * D;
+    const T* pr = P + i * D;
     constexpr int V = kMaxD / 64;
     float uv[V], pv[V];
     float part = 0.f;
 #pragma unroll
     for (int t = 0; t < V; ++t) {
         const int dd = lane + 64 * t;
-        uv[t] = dd < D ? ur[dd] : 0.f;
-        pv[t] = dd < D ? pr[dd] : 0.f;
+        uv[t] = dd < D ? to_f32(ur[dd]) : 0.f;
+        pv[t] = dd < D ? to_f32(pr[dd]) : 0.f;
         part += uv[t] * pv[t];
     }
     // the first NG negative rows stay in registers for the gradient pass
@@ -200,11 +215,11 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
 #pragma unroll
         for (int jj = 0; jj < NG; ++jj) {
             const int j = g0 + jj;
-            const float* qr = a.q + (i * a.n_neg + (j < a.n_neg ? j : 0)) * D;
+            const T* qr = Qn + (i * a.n_neg + (j < a.n_neg ? j : 0)) * D;
 #pragma unroll
             for (int t = 0; t < V; ++t) {
                 const int dd = lane + 64 * t;
-                qv[jj][t] = (j < a.n_neg && dd < D) ? qr[dd] : 0.f;
+                qv[jj][t] = (j < a.n_neg && dd < D) ? to_f32(qr[dd]) : 0.f;
             }
         }
     };
@@ -303,7 +318,7 @@ __device__ __forceinline__ float combine_lse(const float2* part, int n_split, in
 // blockIdx.z = 0: row pass, fixed 32 users, dU += dS · P over the span's items
 // blockIdx.z = 1: column pass, fixed 32 items, dP += dSᵀ · U over the span's users
 // (dS = wb/B·(softmax(S) − I)); one atomic add per output element per span.
-template <int DP>
+template <int DP, typename T>
 __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, bool add_loss) {
     constexpr int DT = DP / 32;
     extern __shared__ __attribute__((aligned(16))) float sm_b[];
@@ -313,8 +328,8 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
     const bool row_pass = blockIdx.z == 0;
     const int64_t f0 = static_cast<int64_t>(blockIdx.x) * RB;    // fixed tile
     const int64_t s0 = static_cast<int64_t>(blockIdx.y) * SPAN;  // streamed span
-    const float* Fm = row_pass ? a.u : a.p;
-    const float* Sm = row_pass ? a.p : a.u;
+    const T* Fm = static_cast<const T*>(row_pass ? a.u : a.p);
+    const T* Sm = static_cast<const T*>(row_pass ? a.p : a.u);
     const float scale = wb_eff / static_cast<float>(a.b);
     float lse_fixed = 0.f;  // row pass: lse of user f0 + c
     const bool ib = wb_eff != 0.f;
@@ -354,10 +369,10 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
 
     float* Ss = sm_b + w * 32 * (DP + LDP);
     float fx[DP / 2];
-    load_fixed<DP>(Fm, f0, a.b, D, fx);
+    load_fixed<DP, T>(Fm, f0, a.b, D, fx);
     const int64_t t0 = s0 + 32 * w, t1 = t0 + 128;
     float4 buf[DP / 8];
-    load_rows<DP>(Sm, t0, a.b, D, buf);
+    load_rows<DP, T>(Sm, t0, a.b, D, buf);
     f32x16 acc[DT];
 #pragma unroll
     for (int x = 0; x < DT; ++x) acc[x] = f32x16{};
@@ -367,7 +382,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
         if (tt >= a.b) break;  // wave-uniform
         store_rows<DP>(Ss, buf);
         wave_lds_sync();
-        if (q == 0 && t1 < a.b) load_rows<DP>(Sm, t1, a.b, D, buf);  // prefetch
+        if (q == 0 && t1 < a.b) load_rows<DP, T>(Sm, t1, a.b, D, buf);  // prefetch
         // st[r]: streamed row tile_row(r,h) x fixed col c
         const f32x16 st = s_tile<DP>(Ss, fx);
         float ds[16];
@@ -446,10 +461,33 @@ void allow_lds(K kernel, size_t bytes) {
     }
 }
 
+template <int DP, typename T>
+int launch_loss(const loss::Args& a, dim3 grid1, dim3 grid2, float wb_eff, hipStream_t st) {
+    const size_t lds = loss::inb_lds_bytes<DP>();
+    allow_lds(loss::loss_fwd_kernel<DP, T>, lds);
+    hipLaunchKernelGGL((loss::loss_fwd_kernel<DP, T>), grid1, dim3(256), lds, st, a);
+    const int rc = check_launch("loss_fwd_kernel");
+    if (rc) return rc;
+    allow_lds(loss::loss_bwd_kernel<DP, T>, lds);
+    hipLaunchKernelGGL((loss::loss_bwd_kernel<DP, T>), grid2, dim3(256), lds, st, a, wb_eff, true);
+    return check_launch("loss_bwd_kernel");
+}
+
+template <typename T>
+int launch_loss_d(const loss::Args& a, int dp32, dim3 grid1, dim3 grid2, float wb_eff, hipStream_t st) {
+    switch (dp32) {
+        case 32: return launch_loss<32, T>(a, grid1, grid2, wb_eff, st);
+        case 64: return launch_loss<64, T>(a, grid1, grid2, wb_eff, st);
+        case 96:
+        case 128: return launch_loss<128, T>(a, grid1, grid2, wb_eff, st);
+        default: return launch_loss<256, T>(a, grid1, grid2, wb_eff, st);
+    }
+}
+
 int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, int d, int n_neg, float inv_tau,
              const float* ub, const float* ib, float we, float wb, double* loss_out, float* du, float* dp,
              float* dq, float* dub, float* dib, void* ws, size_t ws_bytes, void* stream, bool grad) {
-    if (dtype != RT_F32) return RT_ERR_UNSUPPORTED;
+    if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return RT_ERR_INVALID;
     if (b <= 0 || d <= 0 || n_neg < 0 || !u || !p || !loss_out) return RT_ERR_INVALID;
     if (d % 8 != 0 || d > loss::kMaxD || n_neg > loss::kMaxNeg) return RT_ERR_UNSUPPORTED;
     if (n_neg > 0 && !q) return RT_ERR_INVALID;
@@ -463,8 +501,7 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
     const float wb_eff = n_neg > 0 ? wb : 1.f;  // in-batch alone: the loss IS the in-batch CE (weight 1)
     const float we_eff = n_neg > 0 ? we : 0.f;
     const bool want_ib = wb_eff != 0.f;
-    loss::Args a{static_cast<const float*>(u), static_cast<const float*>(p), static_cast<const float*>(q),
-                 b, d, n_neg, inv_tau, ub, ib, we_eff, wb_eff, loss_out, du, dp, dq, dub, dib, part, diag,
+    loss::Args a{u, p, q, b, d, n_neg, inv_tau, ub, ib, we_eff, wb_eff, loss_out, du, dp, dq, dub, dib, part, diag,
                  diag + b, diag + 2 * b, n_split, want_ib ? n_split : 0, grad};
     hipStream_t st = as_stream(stream);
     const unsigned nt = static_cast<unsigned>((b + loss::RB - 1) / loss::RB);
@@ -472,25 +509,11 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
     // forward-only calls still need launch 2's row pass for the loss value
     // launch 2 always runs: its row pass reduces the loss scalars and bias grads
     const dim3 grid1(nt, a.ib_blocks + 8), grid2(nt, want_ib ? n_split : 1, (grad && want_ib) ? 2 : 1);
-#define RT_LOSS(DPV)                                                                                   \
-    do {                                                                                               \
-        const size_t lds = loss::inb_lds_bytes<DPV>();                                                 \
-        allow_lds(loss::loss_fwd_kernel<DPV>, lds);                                                    \
-        hipLaunchKernelGGL(loss::loss_fwd_kernel<DPV>, grid1, dim3(256), lds, st, a);                  \
-        int rc_ = check_launch("loss_fwd_kernel");                                                     \
-        if (rc_) return rc_;                                                                           \
-        allow_lds(loss::loss_bwd_kernel<DPV>, lds);                                                    \
-        hipLaunchKernelGGL(loss::loss_bwd_kernel<DPV>, grid2, dim3(256), lds, st, a, wb_eff, true);    \
-    } while (0)
-    switch (dp32) {
-        case 32: RT_LOSS(32); break;
-        case 64: RT_LOSS(64); break;
-        case 96:
-        case 128: RT_LOSS(128); break;
-        default: RT_LOSS(256); break;
+    switch (dtype) {
+        case RT_F32: return launch_loss_d<float>(a, dp32, grid1, grid2, wb_eff, st);
+        case RT_F16: return launch_loss_d<__half>(a, dp32, grid1, grid2, wb_eff, st);
+        default: return launch_loss_d<__hip_bfloat16>(a, dp32, grid1, grid2, wb_eff, st);
     }
-#undef RT_LOSS
-    return check_launch("loss_bwd_kernel");
 }
 }  // namespace
 

@@ -170,3 +170,38 @@ def sample_negatives(pos_offsets: torch.Tensor, pos_items: torch.Tensor, users: 
         call("rt_sample_negatives", ptr(pos_offsets), ptr(pos_items), pos_offsets.numel() - 1, ptr(users), n,
              num_items, num_neg, seed & 0xFFFFFFFFFFFFFFFF, ptr(seed_offset), ptr(out), stream_of(users))
     return out
+
+
+def twotower_loss(u: torch.Tensor, p: torch.Tensor, q: Optional[torch.Tensor], temperature: float,
+                  user_bias: Optional[torch.Tensor] = None, item_bias: Optional[torch.Tensor] = None,
+                  explicit_weight: float = 0.7, in_batch_weight: float = 0.3, grad: bool = True):
+    """Fused mixed loss (rt_twotower_loss_fwd_bwd / _fwd) on fp32, fp16 or bf16
+    embeddings (widened to fp32 on load). Returns (loss fp64 [3] = (mixed,
+    explicit, in-batch), du, dp, dq, d_user_bias, d_item_bias) — grads fp32 (None
+    without ``grad``). q: [B*N, D] negatives (row i*N+j belongs to user i) or None."""
+    native.require_device(u, p, what="twotower_loss")
+    b, d = u.shape
+    dt = native.dtype_code(u.dtype)
+    if p.dtype != u.dtype or (q is not None and q.dtype != u.dtype):
+        raise TypeError("u, p, q must share a dtype")
+    u, p = u.contiguous(), p.contiguous()
+    q = q.contiguous().reshape(-1, d) if q is not None else None
+    n_neg = q.shape[0] // b if q is not None else 0
+    dev = u.device
+    loss = torch.zeros(3, dtype=torch.float64, device=dev)
+    ws = workspace(dev, native.lib().rt_twotower_loss_workspace_bytes(b, d), "loss_k")
+    f32 = dict(dtype=torch.float32, device=dev)
+    st = stream_of(u)
+    with TIMER.region("loss_fwd_bwd" if grad else "loss_fwd", flops=(6.0 if grad else 2.0) * b * b * d):
+        if grad:
+            du, dp = torch.empty((b, d), **f32), torch.empty((b, d), **f32)
+            dq = torch.empty((q.shape[0], d), **f32) if q is not None else None
+            dub = torch.zeros(1, **f32) if user_bias is not None else None
+            dib = torch.zeros(1, **f32) if item_bias is not None else None
+            call("rt_twotower_loss_fwd_bwd", ptr(u), ptr(p), ptr(q), dt, b, d, n_neg, 1.0 / temperature,
+                 ptr(user_bias), ptr(item_bias), explicit_weight, in_batch_weight, ptr(loss), ptr(du), ptr(dp),
+                 ptr(dq), ptr(dub), ptr(dib), ptr(ws), ws.numel(), st)
+            return loss, du, dp, dq, dub, dib
+        call("rt_twotower_loss_fwd", ptr(u), ptr(p), ptr(q), dt, b, d, n_neg, 1.0 / temperature, ptr(user_bias),
+             ptr(item_bias), explicit_weight, in_batch_weight, ptr(loss), ptr(ws), ws.numel(), st)
+        return loss, None, None, None, None, None
