@@ -18,13 +18,15 @@ def from_db(path):
     return rows
 
 
-def from_csv(path, by_grid=False):
+def from_csv(path, by_grid=False, by_base=False):
     rows = []
     with open(path) as f:
         r = csv.DictReader(f)
         for d in r:
             name = d.get("Kernel_Name") or d.get("KernelName") or d.get("Name")
-            name = name.split("(")[0] if by_grid else name
+            name = name.split("(")[0] if (by_grid or by_base) else name
+            if by_base:  # one row per kernel family: template arguments dropped
+                name = name.split("<")[0].replace("void ", "")
             if by_grid and "Grid_Size_X" in d:
                 name += " grid=%sx%sx%s" % (d["Grid_Size_X"], d["Grid_Size_Y"], d["Grid_Size_Z"])
             if "Start_Timestamp" in d:
@@ -41,8 +43,9 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--title", default="rocprofv3 --kernel-trace summary")
     ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size) = per launch shape")
+    ap.add_argument("--by-base", action="store_true", help="one row per kernel family (all template instances)")
     a = ap.parse_args()
-    rows = from_db(a.src) if a.src.endswith(".db") else from_csv(a.src, a.by_grid)
+    rows = from_db(a.src) if a.src.endswith(".db") else from_csv(a.src, a.by_grid, a.by_base)
     agg = defaultdict(list)
     for name, dur in rows:
         agg[name].append(dur)
