@@ -261,6 +261,18 @@ int rt_twotower_loss_fwd(const void* u, const void* p, const void* q, int dtype,
                          size_t workspace_bytes, void* stream);
 
 /* compute_similarity (src/models/two_tower.py:380-404): s_i = u_i·v_i·inv_tau (+ub+ib). */
+/* In-batch CE of a data-parallel shard (config C5): S = U·Pᵀ/τ over b local
+ * users x n_items in-batch items (all ranks' items, gathered), label of user i =
+ * item label_offset + i; loss_out += (L, 0, L) with L = mean_i CE_i over the
+ * local users (average over ranks for the global mean). du [b, D] and dp
+ * [n_items, D] are OVERWRITTEN with d L / d U, d L / d P (du == NULL: forward
+ * only). Replaces in_batch_negative_loss (src/models/two_tower.py:453-479) for
+ * the sharded case; b == n_items, label_offset == 0 is the reference loss. */
+size_t rt_inbatch_loss_workspace_bytes(int64_t b, int64_t n_items, int d);
+int rt_inbatch_loss_fwd_bwd(const void* u, const void* p, int dtype, int64_t b, int64_t n_items, int d,
+                            int64_t label_offset, float inv_tau, double* loss_out, float* du, float* dp,
+                            void* workspace, size_t workspace_bytes, void* stream);
+
 int rt_similarity_f32(const float* u, const float* v, int64_t b, int d, float inv_tau,
                       const float* user_bias, const float* item_bias, float* out, void* stream);
 

@@ -52,7 +52,9 @@ struct Args {
     float* diag;        // workspace [b]: S_ii = u_i·p_i / tau
     float* expl;        // workspace [b]: explicit CE term lse_i − pos_i
     float* dposv;       // workspace [b]: d loss / d pos_i (= d loss / d bias share of user i)
-    int n_split;        // streamed spans of SPAN rows
+    int64_t nx;         // rows of p (in-batch items); == b for the square reference loss
+    int64_t off;        // label of user i is item off + i (DP shard of a global batch)
+    int n_split;        // streamed spans of SPAN rows (items)
     int ib_blocks;      // launch-1 in-batch block rows (n_split, or 0 without the in-batch term)
     bool grad;
 };
@@ -158,19 +160,19 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
         load_fixed<DP, T>(U, i0, a.b, D, fx);
         const int64_t t0 = static_cast<int64_t>(js) * SPAN + 32 * w, t1 = t0 + 128;
         float4 buf[DP / 8];
-        load_rows<DP, T>(P, t0, a.b, D, buf);
+        load_rows<DP, T>(P, t0, a.nx, D, buf);
         float om = -INFINITY, ol = 0.f;
 #pragma unroll 1
         for (int q = 0; q < 2; ++q) {
             const int64_t tt = q == 0 ? t0 : t1;
-            if (tt >= a.b) break;  // wave-uniform
+            if (tt >= a.nx) break;  // wave-uniform
             store_rows<DP>(Ss, buf);
             wave_lds_sync();
-            if (q == 0 && t1 < a.b) load_rows<DP, T>(P, t1, a.b, D, buf);  // prefetch
+            if (q == 0 && t1 < a.nx) load_rows<DP, T>(P, t1, a.nx, D, buf);  // prefetch
             const f32x16 acc = s_tile<DP>(Ss, fx);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                if (tt + tile_row(r, h) < a.b) {
+                if (tt + tile_row(r, h) < a.nx) {
                     const float sv = acc[r] * a.inv_tau;
                     if (sv > om) { ol = ol * expf(om - sv) + 1.f; om = sv; }
                     else ol += expf(sv - om);
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
     const int64_t i = i0 + 4 * (js - a.ib_blocks) + w;
     if (i >= a.b) return;
     const T* ur = U + i * D;
-    const T* pr = P + i * D;
+    const T* pr = P + (a.off + i) * D;  // the user's positive (its label)
     constexpr int V = kMaxD / 64;
     float uv[V], pv[V];
     float part = 0.f;
@@ -328,6 +330,11 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
     const bool row_pass = blockIdx.z == 0;
     const int64_t f0 = static_cast<int64_t>(blockIdx.x) * RB;    // fixed tile
     const int64_t s0 = static_cast<int64_t>(blockIdx.y) * SPAN;  // streamed span
+    // row pass: fixed users (b), streamed items (nx); column pass: the reverse
+    const int64_t n_fixed = row_pass ? a.b : a.nx, n_str = row_pass ? a.nx : a.b;
+    if (f0 >= n_fixed || s0 >= n_str) {  // grid covers the larger of the two passes
+        if (!(row_pass && blockIdx.y == 0 && f0 < a.b)) return;
+    }
     const T* Fm = static_cast<const T*>(row_pass ? a.u : a.p);
     const T* Sm = static_cast<const T*>(row_pass ? a.p : a.u);
     const float scale = wb_eff / static_cast<float>(a.b);
@@ -362,27 +369,27 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
         }
     } else {
         const int64_t i = s0 + tid;
-        lse_s[tid] = i < a.b ? combine_lse(a.part, a.n_split, a.b, i) : 0.f;
+        lse_s[tid] = i < a.b ? combine_lse(a.part, a.n_split, a.b, i) : 0.f;  // streamed users
     }
     __syncthreads();
-    if (!a.grad || !ib) return;
+    if (!a.grad || !ib || f0 >= n_fixed || s0 >= n_str) return;
 
     float* Ss = sm_b + w * 32 * (DP + LDP);
     float fx[DP / 2];
-    load_fixed<DP, T>(Fm, f0, a.b, D, fx);
+    load_fixed<DP, T>(Fm, f0, n_fixed, D, fx);
     const int64_t t0 = s0 + 32 * w, t1 = t0 + 128;
     float4 buf[DP / 8];
-    load_rows<DP, T>(Sm, t0, a.b, D, buf);
+    load_rows<DP, T>(Sm, t0, n_str, D, buf);
     f32x16 acc[DT];
 #pragma unroll
     for (int x = 0; x < DT; ++x) acc[x] = f32x16{};
 #pragma unroll 1
     for (int q = 0; q < 2; ++q) {
         const int64_t tt = q == 0 ? t0 : t1;
-        if (tt >= a.b) break;  // wave-uniform
+        if (tt >= n_str) break;  // wave-uniform
         store_rows<DP>(Ss, buf);
         wave_lds_sync();
-        if (q == 0 && t1 < a.b) load_rows<DP, T>(Sm, t1, a.b, D, buf);  // prefetch
+        if (q == 0 && t1 < n_str) load_rows<DP, T>(Sm, t1, n_str, D, buf);  // prefetch
         // st[r]: streamed row tile_row(r,h) x fixed col c
         const f32x16 st = s_tile<DP>(Ss, fx);
         float ds[16];
@@ -392,9 +399,11 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
             const int rr = tile_row(r, h);
             const int64_t srow = tt + rr;
             float v = 0.f;
-            if (srow < a.b && fcol < a.b) {
+            if (srow < n_str && fcol < n_fixed) {
                 const float lse = row_pass ? lse_fixed : lse_s[32 * w + 128 * q + rr];
-                v = scale * (expf(st[r] * a.inv_tau - lse) - (srow == fcol ? 1.f : 0.f));
+                // label: item off + user  (row pass: srow item, fcol user; column pass: the reverse)
+                const bool label = row_pass ? (srow == a.off + fcol) : (fcol == a.off + srow);
+                v = scale * (expf(st[r] * a.inv_tau - lse) - (label ? 1.f : 0.f));
             }
             ds[r] = v;
         }
@@ -423,7 +432,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
         const int dt = v >> 4, r = v & 15;
         const int64_t gi = f0 + tile_row(r, l >> 5);
         const int dd = dt * 32 + (l & 31);
-        if (gi < a.b && dd < D) atomicAdd(&out[gi * D + dd], t * a.inv_tau);
+        if (gi < n_fixed && dd < D) atomicAdd(&out[gi * D + dd], t * a.inv_tau);
     }
 }
 
@@ -484,17 +493,24 @@ int launch_loss_d(const loss::Args& a, int dp32, dim3 grid1, dim3 grid2, float w
     }
 }
 
-int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, int d, int n_neg, float inv_tau,
-             const float* ub, const float* ib, float we, float wb, double* loss_out, float* du, float* dp,
-             float* dq, float* dub, float* dib, void* ws, size_t ws_bytes, void* stream, bool grad) {
+size_t loss_ws_bytes(int64_t b, int64_t nx) {
+    const int64_t n_split = (nx + loss::SPAN - 1) / loss::SPAN;
+    return static_cast<size_t>(n_split) * b * sizeof(float2) + 3 * static_cast<size_t>(b) * sizeof(float);
+}
+
+// b users; nx in-batch items (rows of p), label of user i = item off + i
+int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, int64_t nx, int64_t off, int d,
+             int n_neg, float inv_tau, const float* ub, const float* ib, float we, float wb, double* loss_out,
+             float* du, float* dp, float* dq, float* dub, float* dib, void* ws, size_t ws_bytes, void* stream,
+             bool grad) {
     if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return RT_ERR_INVALID;
     if (b <= 0 || d <= 0 || n_neg < 0 || !u || !p || !loss_out) return RT_ERR_INVALID;
+    if (nx < b || off < 0 || off + b > nx) return RT_ERR_INVALID;
     if (d % 8 != 0 || d > loss::kMaxD || n_neg > loss::kMaxNeg) return RT_ERR_UNSUPPORTED;
     if (n_neg > 0 && !q) return RT_ERR_INVALID;
     if (grad && (!du || !dp || (n_neg > 0 && !dq))) return RT_ERR_INVALID;
-    const int n_split = static_cast<int>((b + loss::SPAN - 1) / loss::SPAN);
-    const size_t need = static_cast<size_t>(n_split) * b * sizeof(float2) + 3 * static_cast<size_t>(b) * sizeof(float);
-    if (!ws || ws_bytes < need) return RT_ERR_WORKSPACE;
+    const int n_split = static_cast<int>((nx + loss::SPAN - 1) / loss::SPAN);
+    if (!ws || ws_bytes < loss_ws_bytes(b, nx)) return RT_ERR_WORKSPACE;
     if ((reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(p)) & 15) return RT_ERR_INVALID;
     float2* part = reinterpret_cast<float2*>(ws);
     float* diag = reinterpret_cast<float*>(part + static_cast<size_t>(n_split) * b);
@@ -502,13 +518,20 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
     const float we_eff = n_neg > 0 ? we : 0.f;
     const bool want_ib = wb_eff != 0.f;
     loss::Args a{u, p, q, b, d, n_neg, inv_tau, ub, ib, we_eff, wb_eff, loss_out, du, dp, dq, dub, dib, part, diag,
-                 diag + b, diag + 2 * b, n_split, want_ib ? n_split : 0, grad};
+                 diag + b, diag + 2 * b, nx, off, n_split, want_ib ? n_split : 0, grad};
     hipStream_t st = as_stream(stream);
-    const unsigned nt = static_cast<unsigned>((b + loss::RB - 1) / loss::RB);
+    if (grad && nx != b) {  // dp rows beyond the local users get only column-pass adds
+        if (hipMemsetAsync(dp, 0, static_cast<size_t>(nx) * d * sizeof(float), st) != hipSuccess)
+            return check_launch("hipMemsetAsync(dp)");
+    }
+    const int64_t big = nx > b ? nx : b;
     const int dp32 = (d + 31) / 32 * 32;
-    // forward-only calls still need launch 2's row pass for the loss value
-    // launch 2 always runs: its row pass reduces the loss scalars and bias grads
-    const dim3 grid1(nt, a.ib_blocks + 8), grid2(nt, want_ib ? n_split : 1, (grad && want_ib) ? 2 : 1);
+    // launch 2 always runs: its row pass reduces the loss scalars and bias grads;
+    // its grid covers both passes (fixed tiles of max(b, nx), spans of max(nx, b))
+    const unsigned y2 = static_cast<unsigned>((big + loss::SPAN - 1) / loss::SPAN);
+    const dim3 grid1(static_cast<unsigned>((b + loss::RB - 1) / loss::RB), a.ib_blocks + 8);
+    const dim3 grid2(static_cast<unsigned>((big + loss::RB - 1) / loss::RB), want_ib ? y2 : 1,
+                     (grad && want_ib) ? 2 : 1);
     switch (dtype) {
         case RT_F32: return launch_loss_d<float>(a, dp32, grid1, grid2, wb_eff, st);
         case RT_F16: return launch_loss_d<__half>(a, dp32, grid1, grid2, wb_eff, st);
@@ -520,8 +543,20 @@ int run_loss(const void* u, const void* p, const void* q, int dtype, int64_t b, 
 extern "C" size_t rt_twotower_loss_workspace_bytes(int64_t b, int d) {
     (void)d;
     if (b <= 0) return 256;
-    const int64_t n_split = (b + loss::SPAN - 1) / loss::SPAN;
-    return static_cast<size_t>(n_split) * b * sizeof(float2) + 3 * static_cast<size_t>(b) * sizeof(float) + 256;
+    return loss_ws_bytes(b, b) + 256;
+}
+
+extern "C" size_t rt_inbatch_loss_workspace_bytes(int64_t b, int64_t n_items, int d) {
+    (void)d;
+    if (b <= 0 || n_items < b) return 256;
+    return loss_ws_bytes(b, n_items) + 256;
+}
+
+extern "C" int rt_inbatch_loss_fwd_bwd(const void* u, const void* p, int dtype, int64_t b, int64_t n_items, int d,
+                                       int64_t label_offset, float inv_tau, double* loss_out, float* du, float* dp,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
+    return run_loss(u, p, nullptr, dtype, b, n_items, label_offset, d, 0, inv_tau, nullptr, nullptr, 0.f, 1.f,
+                    loss_out, du, dp, nullptr, nullptr, nullptr, workspace, workspace_bytes, stream, du != nullptr);
 }
 
 
@@ -530,16 +565,16 @@ extern "C" int rt_twotower_loss_fwd_bwd(const void* u, const void* p, const void
                                         float w_explicit, float w_in_batch, double* loss_out, float* du, float* dp,
                                         float* dq, float* d_user_bias, float* d_item_bias, void* workspace,
                                         size_t workspace_bytes, void* stream) {
-    return run_loss(u, p, q, dtype, b, d, n_neg, inv_tau, user_bias, item_bias, w_explicit, w_in_batch, loss_out,
-                    du, dp, dq, d_user_bias, d_item_bias, workspace, workspace_bytes, stream, true);
+    return run_loss(u, p, q, dtype, b, b, 0, d, n_neg, inv_tau, user_bias, item_bias, w_explicit, w_in_batch,
+                    loss_out, du, dp, dq, d_user_bias, d_item_bias, workspace, workspace_bytes, stream, true);
 }
 
 extern "C" int rt_twotower_loss_fwd(const void* u, const void* p, const void* q, int dtype, int64_t b, int d,
                                     int n_neg, float inv_tau, const float* user_bias, const float* item_bias,
                                     float w_explicit, float w_in_batch, double* loss_out, void* workspace,
                                     size_t workspace_bytes, void* stream) {
-    return run_loss(u, p, q, dtype, b, d, n_neg, inv_tau, user_bias, item_bias, w_explicit, w_in_batch, loss_out,
-                    nullptr, nullptr, nullptr, nullptr, nullptr, workspace, workspace_bytes, stream, false);
+    return run_loss(u, p, q, dtype, b, b, 0, d, n_neg, inv_tau, user_bias, item_bias, w_explicit, w_in_batch,
+                    loss_out, nullptr, nullptr, nullptr, nullptr, nullptr, workspace, workspace_bytes, stream, false);
 }
 
 extern "C" int rt_similarity_f32(const float* u, const float* v, int64_t b, int d, float inv_tau,

@@ -15,6 +15,8 @@
   gathers the rows it owns into a dense buffer (zeros elsewhere, via
   ``rt_gather_rows``' row window) and one all-reduce(sum) leaves every row on
   every rank.
+* Data-parallel in-batch step of config C5 (:func:`sharded_inbatch_step`):
+  each rank scores its own users against the whole gathered batch of items.
 * Data-parallel training: the flat fp32 grad slab is averaged with one
   all-reduce (see training/fused_step.py).
 
@@ -120,6 +122,32 @@ def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Te
     rows = gather(table_shard, global_ids, row_begin)
     dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=group)
     return rows
+
+
+def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: torch.Tensor,
+                         item_ids: torch.Tensor, temperature: float, group=None,
+                         gather: Optional[Callable] = None, loss_fn: Optional[Callable] = None):
+    """Config C5 data-parallel in-batch step (SURVEY §8(e) training): the item
+    table is row-sharded, every rank holds ``user_emb`` [b, D] for its own b
+    users and ``item_ids`` [b] of their positives. The global batch's item rows
+    are fetched with :func:`sharded_gather_rows` (one id all-gather + one
+    all-reduce), each rank scores its users against ALL gathered items (label of
+    local user i = global item rank·b + i) with ``rt_inbatch_loss_fwd_bwd``, and
+    the loss is averaged over ranks. Returns (global mean loss, d loss/d user_emb
+    for the local users, d loss/d item rows summed over ranks [B_total, D]) —
+    the latter is what the owners would scatter-add if the table were trainable
+    (in the reference it is a precomputed feature table, so it is not)."""
+    world, rank = _world(group)
+    b = user_emb.shape[0]
+    rows = sharded_gather_rows(table_shard, row_begin, item_ids, group, gather)
+    loss_fn = loss_fn or (lambda u, p, off: kernels.inbatch_loss(u, p, temperature, label_offset=off))
+    loss, du, dp = loss_fn(user_emb, rows, rank * b)
+    lv = loss[0:1].clone()
+    if world > 1:
+        dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(dp, op=dist.ReduceOp.SUM, group=group)
+    # each rank's loss is a mean over its own b users; the global mean averages them
+    return lv / world, du / world, dp / world
 
 
 def allreduce_mean_(t: torch.Tensor, group=None) -> torch.Tensor:

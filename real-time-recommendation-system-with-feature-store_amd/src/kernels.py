@@ -205,3 +205,25 @@ def twotower_loss(u: torch.Tensor, p: torch.Tensor, q: Optional[torch.Tensor], t
         call("rt_twotower_loss_fwd", ptr(u), ptr(p), ptr(q), dt, b, d, n_neg, 1.0 / temperature, ptr(user_bias),
              ptr(item_bias), explicit_weight, in_batch_weight, ptr(loss), ptr(ws), ws.numel(), st)
         return loss, None, None, None, None, None
+
+
+def inbatch_loss(u: torch.Tensor, p: torch.Tensor, temperature: float, label_offset: int = 0,
+                 grad: bool = True):
+    """In-batch CE of b local users against n_items in-batch items (label of user
+    i = item label_offset + i) — rt_inbatch_loss_fwd_bwd. Returns (loss fp64 [3],
+    du [b, D] fp32, dp [n_items, D] fp32); grads None without ``grad``."""
+    native.require_device(u, p, what="inbatch_loss")
+    if u.dtype != p.dtype:
+        raise TypeError("u and p must share a dtype")
+    u, p = u.contiguous(), p.contiguous()
+    b, d = u.shape
+    nx = p.shape[0]
+    dev = u.device
+    loss = torch.zeros(3, dtype=torch.float64, device=dev)
+    ws = workspace(dev, native.lib().rt_inbatch_loss_workspace_bytes(b, nx, d), "inb")
+    du = torch.empty((b, d), dtype=torch.float32, device=dev) if grad else None
+    dp = torch.empty((nx, d), dtype=torch.float32, device=dev) if grad else None
+    with TIMER.region("inbatch_loss", flops=(6.0 if grad else 2.0) * b * nx * d):
+        call("rt_inbatch_loss_fwd_bwd", ptr(u), ptr(p), native.dtype_code(u.dtype), b, nx, d, label_offset,
+             1.0 / temperature, ptr(loss), ptr(du), ptr(dp), ptr(ws), ws.numel(), stream_of(u))
+    return loss, du, dp

@@ -88,6 +88,8 @@ SIGNATURES = {
                                          c_f32, vp, vp, vp, vp, vp, vp, vp, c_size, vp]),
     "rt_twotower_loss_fwd": (c_int, [vp, vp, vp, c_int, c_i64, c_int, c_int, c_f32, vp, vp, c_f32, c_f32,
                                      vp, vp, c_size, vp]),
+    "rt_inbatch_loss_workspace_bytes": (c_size, [c_i64, c_i64, c_int]),
+    "rt_inbatch_loss_fwd_bwd": (c_int, [vp, vp, c_int, c_i64, c_i64, c_int, c_i64, c_f32, vp, vp, vp, vp, c_size, vp]),
     "rt_similarity_f32": (c_int, [vp, vp, c_i64, c_int, c_f32, vp, vp, vp, vp]),
     "rt_grad_sqnorm": (c_int, [vp, vp, c_int, vp, vp, vp, vp]),
     "rt_clip_adam_step": (c_int, [vp, vp, vp, vp, c_i64, vp, c_int, c_f32, c_f32, vp, c_f32, c_f32, c_f32,

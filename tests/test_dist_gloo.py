@@ -5,6 +5,8 @@ per-rank compute bound to the oracle (tests may use the oracle as checker).
 * corpus-sharded exact top-K: merged result == one index over the whole corpus,
   bit-exact on dyadic data (ties resolved by the lower global id);
 * table-sharded gather + all-reduce == one gather from the unsharded table;
+* C5 data-parallel in-batch step (each rank's users vs the gathered global
+  batch, label offset rank·b) == the reference loss and grads of the whole batch;
 * data-parallel gradient average.
 """
 import os
@@ -17,7 +19,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import flat_ip as orc
-from src.dist.sharded import allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_topk
+from src.dist.sharded import (allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_inbatch_step,
+                               sharded_topk)
 
 
 def _free_port():
@@ -127,3 +130,43 @@ def _dp_worker(rank, world):
 
 def test_allreduce_mean_gloo():
     _run(2, _dp_worker)
+
+
+def _c5_worker(rank, world, n, d, b, seed):
+    from oracle import two_tower as orc
+    rng = np.random.default_rng(seed)
+    table = rng.standard_normal((n, d)).astype(np.float32)
+    users = rng.standard_normal((world * b, d)).astype(np.float32)
+    ids = rng.integers(0, n, size=world * b)
+    beg, cnt = shard_range(n, world, rank)
+    shard = torch.from_numpy(table[beg:beg + cnt])
+
+    def window_gather(t, i, begin):
+        loc = i - begin
+        ok = (loc >= 0) & (loc < t.shape[0])
+        out = torch.zeros((i.numel(), t.shape[1]), dtype=t.dtype)
+        out[ok] = t[loc[ok]]
+        return out
+
+    def cpu_loss(u, p, off):  # the reference CE on the local rows, rectangular S, torch autograd
+        uu, pp = u.clone().requires_grad_(), p.clone().requires_grad_()
+        s = uu @ pp.t() / 0.1
+        loss = torch.nn.functional.cross_entropy(s, torch.arange(off, off + u.shape[0]))
+        loss.backward()
+        return torch.stack([loss.detach(), torch.tensor(0.0), loss.detach()]).double(), uu.grad, pp.grad
+
+    u_loc = torch.from_numpy(users[rank * b:(rank + 1) * b])
+    loss, du, dp = sharded_inbatch_step(shard, beg, u_loc, torch.from_numpy(ids[rank * b:(rank + 1) * b]), 0.1,
+                                        gather=window_gather, loss_fn=cpu_loss)
+    # equals the single-process reference loss over the whole global batch
+    U = torch.from_numpy(users).requires_grad_()
+    P = torch.from_numpy(table[ids]).requires_grad_()
+    ref = orc.in_batch_negative_loss(U, P, 0.1)
+    ref.backward()
+    np.testing.assert_allclose(float(loss), float(ref), rtol=1e-6)
+    np.testing.assert_allclose(du.numpy(), U.grad[rank * b:(rank + 1) * b].numpy(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(dp.numpy(), P.grad.numpy(), rtol=1e-5, atol=1e-7)
+
+
+def test_sharded_inbatch_step_gloo():
+    _run(2, _c5_worker, 401, 16, 24, 5)

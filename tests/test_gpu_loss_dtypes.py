@@ -43,3 +43,26 @@ def test_mixed_loss_dtypes(device, dtype, b, d, n_neg):
     if q is not None:
         np.testing.assert_allclose(dq.cpu().numpy(), qq.grad.numpy(), rtol=0,
                                    atol=1e-4 * float(qq.grad.abs().max()))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("world,b,d", [(4, 256, 256), (3, 96, 128)])
+def test_rect_inbatch_loss_equals_sharded_square(device, dtype, world, b, d):
+    """rt_inbatch_loss_fwd_bwd on each simulated rank (b local users vs all
+    world·b items, label offset r·b) averages to the square reference loss."""
+    g = torch.Generator().manual_seed(world * b + d)
+    U = torch.nn.functional.normalize(torch.randn(world * b, d, generator=g), dim=1).to(dtype)
+    P = torch.nn.functional.normalize(torch.randn(world * b, d, generator=g), dim=1).to(dtype)
+    uu, pp = U.float().requires_grad_(), P.float().requires_grad_()
+    ref = orc.in_batch_negative_loss(uu, pp, 0.05)
+    ref.backward()
+    Ud, Pd = U.to(device), P.to(device)
+    tot, dps = 0.0, torch.zeros(world * b, d, device=device)
+    for r in range(world):
+        loss, du, dp = kernels.inbatch_loss(Ud[r * b:(r + 1) * b], Pd, 0.05, label_offset=r * b)
+        tot += loss[0].item() / world
+        dps += dp / world
+        np.testing.assert_allclose((du / world).cpu().numpy(), uu.grad[r * b:(r + 1) * b].numpy(), rtol=0,
+                                   atol=1e-4 * float(uu.grad.abs().max()))
+    np.testing.assert_allclose(tot, ref.item(), rtol=1e-4)
+    np.testing.assert_allclose(dps.cpu().numpy(), pp.grad.numpy(), rtol=0, atol=1e-4 * float(pp.grad.abs().max()))
