@@ -76,12 +76,17 @@ inline Plan make_plan(int64_t nq, int64_t nx, int k, const Shape& sh) {
     p.q_tiles = static_cast<int>((p.chunk + sh.qt - 1) / sh.qt);
     // ~2 blocks per CU (512), but keep >= 4 item tiles per split
     const int64_t tiles = (nx + sh.nt - 1) / sh.nt;
-    int64_t splits = (512 + p.q_tiles - 1) / p.q_tiles;
-    int64_t max_splits = tiles / 4;
-    if (max_splits < 1) max_splits = 1;
-    if (splits > max_splits) splits = max_splits;
-    if (splits > 64) splits = 64;
-    if (splits < 1) splits = 1;
+    int64_t splits;
+    if (sh.kind == 2) {
+        splits = v2::planned_splits(p.q_tiles, nx);
+    } else {
+        splits = (512 + p.q_tiles - 1) / p.q_tiles;
+        int64_t max_splits = tiles / 4;
+        if (max_splits < 1) max_splits = 1;
+        if (splits > max_splits) splits = max_splits;
+        if (splits > 64) splits = 64;
+        if (splits < 1) splits = 1;
+    }
     int64_t tiles_per = (tiles + splits - 1) / splits;
     if (tiles_per < 1) tiles_per = 1;
     p.items_per_split = tiles_per * sh.nt;

@@ -299,13 +299,19 @@ int launch_cfg(const Args& a, const Plan& p, hipStream_t st) {
 }  // namespace rt
 
 #include "topk_v1.h"
+#include "topk_v2.h"
 
 namespace rt {
 namespace topk {
 
-// kernel choice: register lists (this file) for fp32 with k <= 32, the
-// candidate-buffer kernel (topk_v1.h) otherwise. Returns K, or 0 for v1.
-inline int list_k(bool f32, int k) { return (f32 && k <= 16) ? 16 : (f32 && k <= 32) ? 32 : 0; }
+// kernel choice: register lists (this file) for fp32 with k <= 32; the
+// radix-compacted candidate-buffer kernel (topk_v2.h) for 16-bit with
+// k <= 128; the sorted candidate-buffer kernel (topk_v1.h) otherwise.
+// Returns K for the list kernel, 0 for v1, -2 for v2.
+inline int list_k(bool f32, int k) {
+    if (f32) return k <= 16 ? 16 : k <= 32 ? 32 : 0;
+    return k <= v2::kMaxKv2 ? -2 : 0;
+}
 
 template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
@@ -316,6 +322,8 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
             case 32: return launch_cfg<T, S, 32>(a, p, st);
             default: break;
         }
+    } else {
+        if (list_k(false, a.k) == -2) return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
     }
     return v1::launch_S<T, S>(a, p.cap, p.splits, p.items_per_split, st);
 }
@@ -323,13 +331,15 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
 // compile-time shape facts the host planner needs, per (dtype, S)
 struct Shape {
     int qt, nt, cap;
+    int kind;  // 0 register lists, 1 v1, 2 v2
 };
 template <typename T, int S>
 Shape shape_S(int k) {
     switch (list_k(sizeof(T) == 4, k)) {
-        case 16: return {Cfg<T, S, 16>::QT, Cfg<T, S, 16>::NT, 0};
-        case 32: return {Cfg<T, S, 32>::QT, Cfg<T, S, 32>::NT, 0};
-        default: return {v1::kQT, v1::kNT, v1::cap_for(k)};
+        case 16: return {Cfg<T, S, 16>::QT, Cfg<T, S, 16>::NT, 0, 0};
+        case 32: return {Cfg<T, S, 32>::QT, Cfg<T, S, 32>::NT, 0, 0};
+        case -2: return {v2::kQT, v2::kNT, v2::kCap, 2};
+        default: return {v1::kQT, v1::kNT, v1::cap_for(k), 1};
     }
 }
 

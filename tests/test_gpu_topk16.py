@@ -1,0 +1,120 @@
+"""GPU parity of the 16-bit Flat-IP top-K path (f16/bf16, k <= 128: the
+radix-compacted candidate-buffer kernel, csrc/topk_v2.h) against the CPU oracle
+(oracle/flatip.c = faiss.IndexFlatIP.search semantics, src/serving/retrieval.py:
+141-197).
+
+Inputs are dyadic (entries j/64, |j| <= 64): exactly representable in f16 and
+bf16, and every partial sum of a d <= 256 dot product is exact in fp32, so the
+MFMA summation order cannot change a score and the comparison is bit-exact —
+indices included, with the lower id winning exact ties as in Faiss. Corpora
+are large enough that every query's candidate buffer is compacted several
+times (> 480 items per split), and the tie-heavy cases drive the exact-sort
+fallback of the compaction."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import flat_ip as orc
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from src import kernels, native
+    native.lib()
+    return kernels
+
+
+def _dyadic(rng, n, d, lo=-64, hi=64):
+    return (rng.integers(lo, hi + 1, size=(n, d)) / 64.0).astype(np.float32)
+
+
+def _check(K, q, x, k, dtype, exclude=None, id_offset=0):
+    bm_np = None
+    bm = None
+    if exclude is not None:
+        bm_np = orc.exclusion_bitmap(q.shape[0], x.shape[0], exclude)
+        bm = K.exclusion_bitmap(q.shape[0], x.shape[0], exclude, "cuda")
+    rs, ri = orc.flat_ip_search(q, x, k, exclude_bits=bm_np, id_offset=id_offset, nthreads=8)
+    gs, gi = K.flatip_topk(torch.from_numpy(q).to(dtype).cuda(), torch.from_numpy(x).to(dtype).cuda(), k,
+                           exclude_bits=bm, id_offset=id_offset)
+    gi = gi.cpu().numpy()
+    gs = gs.cpu().numpy()
+    bad = np.nonzero((gi != ri).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} rows differ, first {bad[:5]}: got {gi[bad[0]][:8]} want {ri[bad[0]][:8]}"
+    assert np.array_equal(gs, rs)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("nq,nx,d,k", [(300, 20000, 128, 100), (257, 9001, 128, 10), (64, 30000, 128, 128),
+                                       (33, 5000, 128, 1), (100, 12345, 64, 50), (70, 7000, 256, 100),
+                                       (1, 3000, 128, 100), (40, 2500, 96, 64)])
+def test_topk16_dyadic_bit_exact(K, dtype, nq, nx, d, k):
+    rng = np.random.default_rng(nq * 7 + nx + d + k)
+    _check(K, _dyadic(rng, nq, d), _dyadic(rng, nx, d), k, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_topk16_fewer_items_than_k(K, dtype):
+    rng = np.random.default_rng(1)
+    _check(K, _dyadic(rng, 45, 128), _dyadic(rng, 37, 128), 100, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_topk16_massive_exact_ties(K, dtype):
+    """40 distinct rows repeated over 12,000 items: thousands of exact ties per
+    score, so the radix prefix cannot shrink a buffer and the exact-sort
+    fallback (strict threshold, lower id wins) must reproduce Faiss order."""
+    rng = np.random.default_rng(2)
+    base = _dyadic(rng, 40, 128)
+    x = base[rng.integers(0, 40, size=12000)]
+    _check(K, _dyadic(rng, 96, 128), x, 100, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_topk16_coarse_scores(K, dtype):
+    """Small-integer entries: scores take few distinct values (heavy ties at
+    every rank)."""
+    rng = np.random.default_rng(3)
+    q = _dyadic(rng, 80, 64, -1, 1)
+    x = _dyadic(rng, 8000, 64, -1, 1)
+    _check(K, q, x, 128, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_topk16_exclusion_and_offset(K, dtype):
+    rng = np.random.default_rng(4)
+    q = _dyadic(rng, 130, 128)
+    x = _dyadic(rng, 6000, 128)
+    excl = [rng.choice(6000, int(rng.integers(0, 2000)), replace=False) for _ in range(130)]
+    _check(K, q, x, 100, dtype, exclude=excl, id_offset=1_000_000)
+
+
+def test_topk16_c4_shard_properties(K):
+    """C4 shard shape at full size (65,536 queries x 125,000 fp16 rows, k=100):
+    size-independent checks — sorted (score desc, id asc), ids distinct and in
+    range, scores equal to the fp32 dot of the returned rows (recomputed on the
+    device), and a 512-query sample bit-exact against the oracle."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    nq, nx, d, k = 65536, 125000, 128, 100
+    q = torch.randint(-64, 65, (nq, d), device="cuda", generator=g).half() / 64
+    x = torch.randint(-64, 65, (nx, d), device="cuda", generator=g).half() / 64
+    gs, gi = K.flatip_topk(q, x, k)
+    torch.cuda.synchronize()
+    assert (gi >= 0).all() and (gi < nx).all()
+    assert (gs[:, :-1] >= gs[:, 1:]).all()
+    tie = gs[:, :-1] == gs[:, 1:]
+    assert (gi[:, :-1][tie] < gi[:, 1:][tie]).all()
+    srt = gi.sort(dim=1).values
+    assert (srt[:, 1:] != srt[:, :-1]).all()
+    rows = x.float()[gi[:4096]]                       # [4096, k, d]
+    dots = torch.einsum("qkd,qd->qk", rows, q[:4096].float())
+    assert torch.equal(dots, gs[:4096])
+    sel = torch.randperm(nq, generator=torch.Generator().manual_seed(0))[:512].numpy()
+    qs = q.float().cpu().numpy()[sel]
+    rs, ri = orc.flat_ip_search(np.ascontiguousarray(qs), x.float().cpu().numpy(), k, nthreads=16)
+    assert np.array_equal(gi.cpu().numpy()[sel], ri)
+    assert np.array_equal(gs.cpu().numpy()[sel], rs)
