@@ -12,10 +12,13 @@
 //   store at the lane's own counter — no atomics, no cross-lane slot math. Hot
 //   filter per lane = max of its 16 scores against the query's threshold; a
 //   sub-tile whose wave has no passing lane costs ~12 VALU.
-// * the item-tile prefetch is issued as untracked inline-asm loads and waited
-//   for with a vmcnt bound derived from the number of candidate stores issued
-//   after it (wave-uniform), so staging the next tile never waits for the
-//   appends' store acknowledgements.
+// * item tiles arrive by LDS-DMA (global_load_lds_dwordx4, inline asm: no VGPR
+//   destination) into a lane-linear image whose 16-byte chunks are XOR-swizzled
+//   per row through the SOURCE address, so the A-fragment ds_read_b128 are
+//   conflict-free; the next tile's DMA is issued at the top of an iteration and
+//   waited for before the raw barrier at its end with a vmcnt bound derived
+//   from the (wave-uniform) number of candidate stores issued after it — never
+//   a blanket vmcnt(0), so appends' store acknowledgements are not waited for.
 // * compaction when a buffer nears capacity: a two-pass 8-bit radix select on
 //   order-preserving keys (per-wave LDS histogram) finds a 16-bit key prefix T
 //   with >= k entries at or above it; entries below T can never reach the top
@@ -33,7 +36,7 @@ namespace v2 {
 
 constexpr int kWavesB = 8;            // waves per block
 constexpr int kQT = 32 * kWavesB;     // queries per block
-constexpr int kNT = 64;               // items per LDS stage
+constexpr int kNT = 128;              // items per LDS stage
 constexpr int kCap = 512;             // candidate entries per query
 constexpr int kHalf = kCap / 2;       // per owning lane
 constexpr int kE = kCap / 64;         // entries per lane in a compaction
@@ -184,13 +187,6 @@ __device__ __noinline__ void emit_sorted(const Cand* __restrict__ buf, int n0, i
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// 16-byte global load the compiler does not track: its destination is only
-// valid after an explicit vmcnt wait (wait_vm_le)
-__device__ __forceinline__ u32x4 load_untracked(const void* p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
 // wait until at most n (wave-uniform, >= 0) vector-memory operations are in
 // flight, rounded down to a power of two
 __device__ __forceinline__ void wait_vm_le(int n) {
@@ -208,10 +204,30 @@ struct Cfg2 {
     static constexpr int KK = Mfma<T>::kK;                      // 16
     static constexpr int DP = S * KK;                            // padded d
     static constexpr int VEC = 16 / static_cast<int>(sizeof(T));  // 8 elements per 16 B
-    static constexpr int LS = DP + VEC;                          // +16 B pad per row
-    static constexpr int TILE_VECS = kNT * (DP / VEC);
-    static constexpr int LOADS = (TILE_VECS + 64 * kWavesB - 1) / (64 * kWavesB);
+    static constexpr int ROWB = DP * static_cast<int>(sizeof(T));   // bytes per LDS row (unpadded)
+    static constexpr int P = ROWB / 16;                              // 16-byte chunks per row
+    static constexpr int TILE_BYTES = kNT * ROWB;
+    static constexpr int DMA_PER_WAVE = TILE_BYTES / 1024 / kWavesB;  // 1 KiB per wave-instruction
+    static_assert(DMA_PER_WAVE * 1024 * kWavesB == TILE_BYTES, "tile must split into whole DMA pieces");
+    // chunk swizzle of row r: distinct bank groups for the 16 rows a ds_read_b128 lane group touches
+    __device__ static int swz(int r) { return P >= 16 ? (r & 15) : ((r / (16 / P)) & (P - 1)); }
 };
+
+static __device__ const uint4 kZero16 = {0u, 0u, 0u, 0u};
+
+template <typename P>
+__device__ __forceinline__ uint32_t lds_addr(P* p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)(p)));
+}
+// one LDS-DMA piece: each lane's 16 bytes from gsrc land at lds_dst + 16 * lane
+// (M0 carries the wave-uniform destination; saved and restored in the statement)
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
 
 // grid: 1-D, block b → (query tile b / splits, item split b % splits); with
 // splits | 8 every XCD (b mod 8) streams one split of the corpus.
@@ -219,8 +235,8 @@ template <typename T, int S, bool EXCL>
 __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits, int64_t items_per_split) {
     using M = Mfma<T>;
     using C = Cfg2<T, S>;
-    constexpr int DP = C::DP, LS = C::LS, VEC = C::VEC, TILE_VECS = C::TILE_VECS, LOADS = C::LOADS;
-    __shared__ __attribute__((aligned(16))) T tile[2][kNT * LS];
+    constexpr int DP = C::DP, VEC = C::VEC, ROWB = C::ROWB;
+    __shared__ __attribute__((aligned(1024))) T tile[2][C::TILE_BYTES / sizeof(T)];
     __shared__ __attribute__((aligned(16))) uint32_t hist[kWavesB][256];
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
@@ -262,35 +278,33 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     float thr = qok ? -FLT_MAX : INFINITY;
     int cnt = 0;
 
-    // prefetch registers: one tile, zero padded past d; rows past the split
-    // end load a clamped (valid) row — their scores are masked to -inf
-    u32x4 pre[LOADS];
-    int vm_after = 0;  // VMEM instructions issued since the prefetch (wave-uniform); >= 1<<20: drained
-    auto fetch = [&](int64_t t0) {
+    // LDS-DMA of one tile (rows t0 .., zero chunks past d; rows past the split
+    // end read a clamped valid row — their scores are masked to -inf)
+    int vm_after = 0;  // VMEM instructions issued since the last DMA (wave-uniform); >= 1<<20: drained
+    const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
+    auto fetch = [&](int64_t t0, int buf) {
+        const uint32_t base = lds_addr(&tile[buf][0]) + wave_u * (C::DMA_PER_WAVE * 1024);
 #pragma unroll
-        for (int l = 0; l < LOADS; ++l) {
-            const int e = tid + l * 64 * kWavesB;
-            const int r = e / (DP / VEC);
-            const int c = e % (DP / VEC);
+        for (int j = 0; j < C::DMA_PER_WAVE; ++j) {
+            const int o = (wave * C::DMA_PER_WAVE + j) * 1024 + lane * 16;
+            const int r = o / ROWB;
+            const int c = ((o % ROWB) >> 4) ^ C::swz(r);
             int64_t item = t0 + r;
             item = item < i_end ? item : i_end - 1;
-            if (e < TILE_VECS && c < row_vecs) pre[l] = load_untracked(X + item * d + c * VEC);
+            const void* src = c < row_vecs ? static_cast<const void*>(X + item * d + c * VEC)
+                                           : static_cast<const void*>(&kZero16);
+            glds16(src, base + j * 1024);
         }
         vm_after = 0;
     };
-    auto stage = [&](int buf) {
+    // the DMA into the other buffer has landed (its count bound is exact or drained)
+    auto fetch_wait = [&]() {
         if (vm_after < (1 << 20)) wait_vm_le(vm_after);
-#pragma unroll
-        for (int l = 0; l < LOADS; ++l) {
-            const int e = tid + l * 64 * kWavesB;
-            if (e < TILE_VECS) {
-                const int r = e / (DP / VEC);
-                const int c = e % (DP / VEC);
-                u32x4 v = pre[l];
-                if (c >= row_vecs) v = u32x4{0u, 0u, 0u, 0u};
-                *reinterpret_cast<u32x4*>(&tile[buf][r * LS + c * VEC]) = v;
-            }
-        }
+    };
+    auto raw_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     };
 
     // select from one 32-item sub-tile's scores (acc[r] = item sub0 + tile_row(r, half), query col)
@@ -335,25 +349,26 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     };
 
     if (i_begin < i_end) {
-        fetch(i_begin);
-        vm_after = 0;
-        stage(0);
-        if (i_begin + kNT < i_end) fetch(i_begin + kNT);
+        fetch(i_begin, 0);
+        wait_vm_le(0);
     }
-    __syncthreads();
+    raw_barrier();
     int cur = 0;
     for (int64_t t0 = i_begin; t0 < i_end; t0 += kNT) {
         const T* tl = tile[cur];
         const bool more = t0 + kNT < i_end;
+        // the next tile's DMA: buffer cur^1 was last read before the previous barrier
+        if (more) fetch(t0 + kNT, cur ^ 1);
 #pragma unroll
         for (int rt = 0; rt < kNT / 32; ++rt) {
             const int64_t sub0 = t0 + rt * 32;
             if (sub0 >= i_end) break;  // block-uniform
             f32x16 acc = {};
-            const T* arow = tl + (rt * 32 + col) * LS + 8 * half;
+            const int row = rt * 32 + col;
+            const T* arow = tl + row * DP;
             typename M::frag af[S];
 #pragma unroll
-            for (int s = 0; s < S; ++s) af[s] = frag_from<T>(arow + s * 16);
+            for (int s = 0; s < S; ++s) af[s] = frag_from<T>(arow + ((2 * s + half) ^ C::swz(row)) * VEC);
 #pragma unroll
             for (int s = 0; s < S; ++s) acc = M::run(af[s], qf[s], acc);
             if (sub0 + 32 > i_end) {  // rows past the end never qualify
@@ -362,16 +377,11 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
                 for (int r = 0; r < 16; ++r)
                     if (tile_row(r, half) >= left) acc[r] = -INFINITY;
             }
-            if (rt == kNT / 32 - 1 && more) {
-                // stage the next tile before this sub-tile's appends: the wait
-                // for the prefetch then covers only the earlier sub-tiles' stores
-                stage(cur ^ 1);
-                if (t0 + 2 * kNT < i_end) fetch(t0 + 2 * kNT);
-            }
             select(acc, sub0);
             maybe_compact();
         }
-        __syncthreads();
+        if (more) fetch_wait();
+        raw_barrier();
         cur ^= 1;
     }
 
