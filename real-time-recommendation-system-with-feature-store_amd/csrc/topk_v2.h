@@ -36,7 +36,7 @@ namespace v2 {
 
 constexpr int kWavesB = 8;            // waves per block
 constexpr int kQT = 32 * kWavesB;     // queries per block
-constexpr int kNT = 128;              // items per LDS stage
+constexpr int kNT = 128;              // split granularity; items per LDS stage: Cfg2::NT
 constexpr int kCap = 512;             // candidate entries per query
 constexpr int kHalf = kCap / 2;       // per owning lane
 constexpr int kE = kCap / 64;         // entries per lane in a compaction
@@ -206,7 +206,8 @@ struct Cfg2 {
     static constexpr int VEC = 16 / static_cast<int>(sizeof(T));  // 8 elements per 16 B
     static constexpr int ROWB = DP * static_cast<int>(sizeof(T));   // bytes per LDS row (unpadded)
     static constexpr int P = ROWB / 16;                              // 16-byte chunks per row
-    static constexpr int TILE_BYTES = kNT * ROWB;
+    static constexpr int NT = S <= 8 ? 128 : 64;                    // items per LDS stage
+    static constexpr int TILE_BYTES = NT * ROWB;
     static constexpr int DMA_PER_WAVE = TILE_BYTES / 1024 / kWavesB;  // 1 KiB per wave-instruction
     static_assert(DMA_PER_WAVE * 1024 * kWavesB == TILE_BYTES, "tile must split into whole DMA pieces");
     // chunk swizzle of row r: distinct bank groups for the 16 rows a ds_read_b128 lane group touches
@@ -238,6 +239,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     constexpr int DP = C::DP, VEC = C::VEC, ROWB = C::ROWB;
     __shared__ __attribute__((aligned(1024))) T tile[2][C::TILE_BYTES / sizeof(T)];
     __shared__ __attribute__((aligned(16))) uint32_t hist[kWavesB][256];
+    __shared__ __attribute__((aligned(16))) float scr[kWavesB * 64 * 20];  // per-lane score rows (80 B: conflict-free b128)
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
     const T* __restrict__ X = reinterpret_cast<const T*>(a.X);
@@ -256,6 +258,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32 buffers
     Cand* const mybuf = cbase + static_cast<int64_t>(col) * kCap + half * kHalf;  // this lane's half
     uint32_t* const whist = hist[wave];
+    float* const wscr = scr + (wave * 64 + lane) * 20;
 
     typename M::frag qf[S];
     {
@@ -313,17 +316,39 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
 #pragma unroll
         for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[r]);
         if (__ballot(m >= thr) == 0) return;
-        uint32_t xw = 0u;  // sub0 is 32-aligned: one bitmap word per sub-tile
-        if constexpr (EXCL) xw = excl ? excl[sub0 >> 5] : 0u;
+        // per-lane pass mask, 2 VALU per score: bit 15-r <=> acc[r] passes
+        uint32_t bits = 0u;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int row = tile_row(r, half);
-            bool p = acc[r] >= thr;
-            if constexpr (EXCL) p = p && !((xw >> row) & 1u);
-            if (__ballot(p) == 0) continue;
+        for (int r = 0; r < 16; ++r)
+            asm("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+                : "+v"(bits)
+                : "v"(acc[r]), "v"(thr)
+                : "vcc");
+        if constexpr (EXCL) {
+            if (excl) {
+                const uint32_t xw = excl[sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if ((xw >> tile_row(r, half)) & 1u) bits &= ~(1u << (15 - r));
+            }
+        }
+        // the lane's scores go through its LDS scratch row so the append loop
+        // can index them; the wave loops max-popcount times (1-2 late in a scan)
+        if (bits) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<float4*>(wscr + 4 * i) =
+                    make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        }
+        wave_lds_sync();
+        while (__ballot(bits != 0u)) {
             ++vm_after;  // one store instruction for the wave
-            if (p) {
-                mybuf[cnt] = Cand{acc[r], static_cast<uint32_t>(sub0 + row)};
+            if (bits) {
+                const int b = 31 - __builtin_clz(bits);  // highest set bit = lowest r
+                bits &= ~(1u << b);
+                const int r = 15 - b;
+                const float v = wscr[r];
+                mybuf[cnt] = Cand{v, static_cast<uint32_t>(sub0 + tile_row(r, half))};
                 ++cnt;
             }
         }
@@ -354,13 +379,14 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     }
     raw_barrier();
     int cur = 0;
-    for (int64_t t0 = i_begin; t0 < i_end; t0 += kNT) {
+    constexpr int NT = C::NT;
+    for (int64_t t0 = i_begin; t0 < i_end; t0 += NT) {
         const T* tl = tile[cur];
-        const bool more = t0 + kNT < i_end;
+        const bool more = t0 + NT < i_end;
         // the next tile's DMA: buffer cur^1 was last read before the previous barrier
-        if (more) fetch(t0 + kNT, cur ^ 1);
+        if (more) fetch(t0 + NT, cur ^ 1);
 #pragma unroll
-        for (int rt = 0; rt < kNT / 32; ++rt) {
+        for (int rt = 0; rt < NT / 32; ++rt) {
             const int64_t sub0 = t0 + rt * 32;
             if (sub0 >= i_end) break;  // block-uniform
             f32x16 acc = {};
