@@ -196,12 +196,10 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
         row_ok[i] = nn < n;
         wrow[i] = a.w + static_cast<int64_t>(row_ok[i] ? nn : 0) * k;
     }
-    // 16 k-steps per iteration (kh % 16 == 0): all loads issued before the MFMAs
-    for (int s = 0; s < kh; s += 16) {
-        float4 av[4];
-        float4 wv[TPW][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) av[j] = *reinterpret_cast<const float4*>(ap + s + 4 * j);
+    // 16 k-steps per iteration (kh % 16 == 0); the W fragments of the next
+    // iteration are loaded during this one's MFMAs (register double buffer)
+    float4 wv[TPW][4], wn[TPW][4];
+    auto load_w = [&](int s, float4 (&dst)[TPW][4]) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
 #pragma unroll
@@ -219,8 +217,19 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
                         if (kk + 3 < k) v.w = wr[3];
                     }
                 }
-                wv[i][j] = v;
+                dst[i][j] = v;
             }
+    };
+    load_w(0, wn);
+    for (int s = 0; s < kh; s += 16) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wv[i][j] = wn[i][j];
+        if (s + 16 < kh) load_w(s + 16, wn);
+        float4 av[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) av[j] = *reinterpret_cast<const float4*>(ap + s + 4 * j);
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             if (!tile_on[i]) continue;
@@ -447,11 +456,9 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) acc[i] = f32x16{};
     const float* dp = Dz + c32 * ldz + h * nh;
-    for (int s = 0; s < nh; s += 8) {  // 8 k-steps per iteration (nh % 16 == 0)
-        float4 av[2];
-        float wv[TPWK][8];
-        av[0] = *reinterpret_cast<const float4*>(dp + s);
-        av[1] = *reinterpret_cast<const float4*>(dp + s + 4);
+    // 8 k-steps per iteration (nh % 16 == 0); next iteration's W loaded during this one's MFMAs
+    float wv[TPWK][8], wn[TPWK][8];
+    auto load_w = [&](int s, float (&dst)[TPWK][8]) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
             const int kk = (w + 4 * i) * 32 + c32;
@@ -459,9 +466,20 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int nn = h * nh + s + j;
-                wv[i][j] = (on && nn < n) ? a.w[static_cast<int64_t>(nn) * k + kk] : 0.f;
+                dst[i][j] = (on && nn < n) ? a.w[static_cast<int64_t>(nn) * k + kk] : 0.f;
             }
         }
+    };
+    load_w(0, wn);
+    for (int s = 0; s < nh; s += 8) {
+#pragma unroll
+        for (int i = 0; i < TPWK; ++i)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) wv[i][j] = wn[i][j];
+        if (s + 8 < nh) load_w(s + 8, wn);
+        float4 av[2];
+        av[0] = *reinterpret_cast<const float4*>(dp + s);
+        av[1] = *reinterpret_cast<const float4*>(dp + s + 4);
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
             if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
