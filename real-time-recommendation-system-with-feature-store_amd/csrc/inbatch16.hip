@@ -1,0 +1,501 @@
+// In-batch-negative cross-entropy on 16-bit embeddings (config C5: bf16, D=256)
+// with the scores on the 16-bit MFMA (v_mfma_f32_32x32x16_{bf16,f16}).
+//
+// Replaces, for 16-bit U/P and no explicit negatives,
+//   in_batch_negative_loss (src/models/two_tower.py:453-479):
+//     S = U·Pᵀ/τ ; L = mean_i CE(S_i, label off+i)
+//   and its autograd backward  dU = dS·P/τ, dP = dSᵀ·U/τ, dS = (softmax(S) − I)/b.
+// 16-bit × 16-bit products are exact in fp32 and the MFMA accumulates in fp32,
+// so S equals the widened fp32 product up to summation order. dS is fp32; it
+// enters the gradient MFMAs as a 16-bit hi + lo pair (bf16: to 2^-17 relative;
+// f16 after a 2^15 scale that keeps small probabilities out of underflow), so
+// the gradients keep close to fp32 accuracy.
+//
+// Three launches, flash-attention style (S is never stored):
+//   lse  : fixed 32 users per wave (B operand in registers), items streamed
+//          through LDS; online base-2 log-sum-exp per user and item split.
+//   row  : same geometry; S recomputed, dS formed in registers and used, with
+//          no lane movement, as the B operand of dUᵀ += Pᵀ·dS (the accumulator
+//          layout of S IS the k-permuted operand layout); Pᵀ fragments come
+//          from the same LDS image by ds_read_b64_tr_b16 (transposed reads).
+//   col  : the mirror: fixed 32 items per wave, users streamed; dPᵀ += Uᵀ·dS.
+// Item/user tiles arrive by LDS-DMA into a [NT][128-col] image per 128-column
+// half whose 16-byte chunks are XOR-swizzled so that both the row reads
+// (ds_read_b128) and the transposed reads are bank-conflict free.
+// Gradient partials of each split are summed by a fixed-order reduce launch
+// (deterministic, no atomics).
+#include <float.h>
+
+#include "rt_common.h"
+
+namespace rt {
+namespace ib16 {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 64;            // streamed rows per LDS stage
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <typename T> struct M16;
+template <> struct M16<__hip_bfloat16> {
+    __device__ static f32x16 run(s16x8 a, s16x8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(__attribute__((ext_vector_type(8))) __bf16, a),
+                                                       __builtin_bit_cast(__attribute__((ext_vector_type(8))) __bf16, b),
+                                                       c, 0, 0, 0);
+    }
+};
+template <> struct M16<__half> {
+    __device__ static f32x16 run(s16x8 a, s16x8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(__attribute__((ext_vector_type(8))) _Float16, a),
+                                                      __builtin_bit_cast(__attribute__((ext_vector_type(8))) _Float16, b),
+                                                      c, 0, 0, 0);
+    }
+};
+
+__device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// ---- LDS image: per 128-column half, [NT rows][16 chunks of 16 B], chunk
+// index XOR-swizzled by row (conflict-free row reads AND tr_b16 reads)
+__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int img_off(int half, int row, int ch) {
+    return half * (NT * 256) + row * 256 + ((ch ^ swz(row)) << 4);
+}
+
+static __device__ const uint4 kZero16 = {0u, 0u, 0u, 0u};
+
+template <typename P>
+__device__ __forceinline__ uint32_t lds_addr(P* p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) char*)(p)));
+}
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_dst)
+                 : "memory");
+}
+// transposed LDS read (ds_read_b64_tr_b16): for the 16-lane group of this lane,
+// lane 4q+p addresses row q / columns 4p..4p+3 of a 4 x 16 block; lane i gets column i
+__device__ __forceinline__ s16x4 tr_read(const char* lds, int byte_off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(lds + byte_off));
+}
+
+// x → (hi, lo) 16-bit pair with x ≈ hi + lo; two elements packed per dword (lo element first)
+template <typename T> struct Split;
+template <> struct Split<__hip_bfloat16> {
+    static constexpr float kScale = 1.f;  // bf16 keeps the fp32 exponent range
+    __device__ static void run(float x0, float x1, uint32_t& hp, uint32_t& lp) {
+        const __hip_bfloat16 h0 = __float2bfloat16(x0), h1 = __float2bfloat16(x1);
+        const __hip_bfloat16 l0 = __float2bfloat16(x0 - __bfloat162float(h0));
+        const __hip_bfloat16 l1 = __float2bfloat16(x1 - __bfloat162float(h1));
+        hp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
+        lp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l1)) << 16);
+    }
+};
+template <> struct Split<__half> {
+    static constexpr float kScale = 32768.f;  // dS·2^15 keeps small probabilities out of f16 underflow
+    __device__ static void run(float x0, float x1, uint32_t& hp, uint32_t& lp) {
+        const __half h0 = __float2half_rn(x0), h1 = __float2half_rn(x1);
+        const __half l0 = __float2half_rn(x0 - __half2float(h0));
+        const __half l1 = __float2half_rn(x1 - __half2float(h1));
+        hp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
+        lp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l1)) << 16);
+    }
+};
+
+enum Pass { LSE = 0, ROW = 1, COL = 2 };
+
+struct Args {
+    const void* fixed;    // rows held as B operand (users for LSE/ROW, items for COL)
+    const void* stream;   // rows streamed through LDS
+    int64_t n_fixed, n_stream;
+    int d;
+    int64_t off;          // label of user i is item off + i
+    float c2;             // inv_tau * log2(e): base-2 logits
+    float inv_tau;
+    float w;              // d L / d CE_i = 1 / b
+    int splits;
+    int64_t per_split;    // streamed rows per split (multiple of NT)
+    float2* part;         // LSE: [splits][n_fixed] (max2, sum) base 2
+    float* diag2;         // LSE: [n_fixed] x_ii (base-2 logit of the label)
+    const float* lse2;    // ROW/COL: [b] base-2 log-sum-exp per user
+    float* gpart;         // ROW/COL: [splits][n_fixed][DP] gradient partials
+};
+
+template <int DP, int PASS> struct Geo {
+    static constexpr int S16 = DP / 16;                 // 16-wide k-steps of a dot
+    // gradient passes at DP=256 hold 8 accumulator tiles (128 registers): one
+    // wave per SIMD with the 512-register file; everything else two per SIMD
+    static constexpr int WAVES = (PASS != 0 && DP > 128) ? 4 : 8;
+    static constexpr int DSPLIT = 1;
+    static constexpr int DB = DP / 32 / DSPLIT;         // 32-wide d blocks per wave
+    static constexpr int FT = 32 * WAVES / DSPLIT;      // fixed rows per block
+    static constexpr int TILE_BYTES = NT * DP * 2;
+    static constexpr int DMA_PER_WAVE = TILE_BYTES / 1024 / WAVES;
+    static_assert(DMA_PER_WAVE * 1024 * WAVES == TILE_BYTES, "tile must split into whole DMA pieces");
+};
+
+template <typename T, int DP, int PASS>
+__global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args a) {
+    using G = Geo<DP, PASS>;
+    using MM = M16<T>;
+    constexpr int S16 = G::S16;
+    __shared__ __attribute__((aligned(1024))) char tile[2][G::TILE_BYTES];
+    __shared__ __attribute__((aligned(16))) float tlse[2][NT];  // COL: lse2 of the streamed users
+
+    const T* __restrict__ F = reinterpret_cast<const T*>(a.fixed);
+    const T* __restrict__ X = reinterpret_cast<const T*>(a.stream);
+    const int d = a.d;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 31, h = lane >> 5;
+    const int split = static_cast<int>(blockIdx.x % static_cast<unsigned>(a.splits));
+    const int64_t fblk = blockIdx.x / static_cast<unsigned>(a.splits);
+    const int64_t fw = fblk * G::FT + (wave / G::DSPLIT) * 32;  // wave's first fixed row
+    const int db0 = (wave % G::DSPLIT) * G::DB;                 // first d block of this wave's gradient
+    const int64_t f = fw + col;                     // this lane's fixed row (its MFMA column)
+    const bool fok = f < a.n_fixed;
+    const int64_t i_begin = static_cast<int64_t>(split) * a.per_split;
+    const int64_t i_end = (i_begin + a.per_split) < a.n_stream ? (i_begin + a.per_split) : a.n_stream;
+    const int row_vecs = d / 8;
+
+    // fixed-row fragments: B[k = 16s + 8h + j][col]
+    s16x8 qf[S16];
+    {
+        const T* fr = F + (fok ? f : 0) * d;
+#pragma unroll
+        for (int s = 0; s < S16; ++s) {
+            const int k0 = 16 * s + 8 * h;
+            if (fok && k0 < d) qf[s] = __builtin_bit_cast(s16x8, *reinterpret_cast<const uint4*>(fr + k0));
+            else qf[s] = s16x8{};
+        }
+    }
+
+    // per-pass state
+    float run_m = -INFINITY, run_s = 0.f, dg = 0.f;  // LSE (base 2), diag
+    float lse_f = 0.f;                                // ROW: the user's lse2
+    f32x16 gacc[G::DB];                               // ROW/COL: gradient tile per 32-col d block
+    if constexpr (PASS != LSE) {
+#pragma unroll
+        for (int i = 0; i < G::DB; ++i) gacc[i] = f32x16{};
+    }
+    if constexpr (PASS == ROW) lse_f = fok ? a.lse2[f] : 0.f;
+
+    const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
+    auto fetch = [&](int64_t t0, int buf) {
+        const uint32_t base = lds_addr(&tile[buf][0]) + wave_u * (G::DMA_PER_WAVE * 1024);
+#pragma unroll
+        for (int j = 0; j < G::DMA_PER_WAVE; ++j) {
+            const int o = (wave * G::DMA_PER_WAVE + j) * 1024 + lane * 16;
+            const int half = o / (NT * 256);
+            const int oo = o - half * (NT * 256);
+            const int r = oo >> 8;
+            const int c = half * 16 + (((oo & 255) >> 4) ^ swz(r));  // global 16-B chunk of the row
+            int64_t item = t0 + r;
+            item = item < i_end ? item : i_end - 1;
+            const void* src = c < row_vecs ? static_cast<const void*>(X + item * d + c * 8)
+                                           : static_cast<const void*>(&kZero16);
+            glds16(src, base + j * 1024);
+        }
+        if constexpr (PASS == COL) {  // 64 lse2 values: 16 lanes x 16 B (the array is padded to 64)
+            if (wave == 0 && lane < NT / 4) glds16(a.lse2 + t0 + 4 * lane, lds_addr(&tlse[buf][0]));
+        }
+    };
+    auto raw_barrier = [&]() {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    if (i_begin < i_end) fetch(i_begin, 0);
+    raw_barrier();
+    int cur = 0;
+    for (int64_t t0 = i_begin; t0 < i_end; t0 += NT) {
+        const char* tl = tile[cur];
+        if (t0 + NT < i_end) fetch(t0 + NT, cur ^ 1);
+#pragma unroll
+        for (int rt = 0; rt < NT / 32; ++rt) {
+            const int64_t sub0 = t0 + rt * 32;
+            if (sub0 >= i_end) break;  // block-uniform
+            // ---- S tile: acc[r] = <stream row sub0 + tile_row(r,h), fixed row f> ----
+            f32x16 acc = {};
+            {
+                const int row = rt * 32 + col;
+#pragma unroll
+                for (int s = 0; s < S16; ++s) {
+                    const int cg = 2 * s + h;
+                    const s16x8 af = __builtin_bit_cast(
+                        s16x8, *reinterpret_cast<const uint4*>(tl + img_off(cg >> 4, row, cg & 15)));
+                    acc = MM::run(af, qf[s], acc);
+                }
+            }
+            const int left = static_cast<int>(i_end - sub0 < 32 ? i_end - sub0 : 32);
+            if constexpr (PASS == LSE) {
+                float x[16];
+                float mx = -INFINITY;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    x[r] = tile_row(r, h) < left ? acc[r] * a.c2 : -INFINITY;
+                    mx = fmaxf(mx, x[r]);
+                }
+                const float mn = fmaxf(run_m, mx);
+                float s = run_s * exp2f(run_m - mn);
+                if (mn == -INFINITY) s = 0.f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s += exp2f(x[r] - mn);
+                run_m = mn;
+                run_s = s;
+                // label column: stream row f + off
+                const int64_t rr = f + a.off - sub0;
+                if (fok && rr >= 0 && rr < 32 && ((rr >> 2) & 1) == h) {
+                    const int rsel = static_cast<int>((rr & 3) + 4 * (rr >> 3));
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (r == rsel) dg = x[r];
+                }
+            } else {
+                // ---- dS = w·(2^(x − lse2_user) − [label]) in registers, as bf16 hi + lo ----
+                float lse_r[16];
+                if constexpr (PASS == COL) {  // users are the streamed rows: lse2 per row, from LDS
+                    const float* tls = tlse[cur] + rt * 32;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 v = *reinterpret_cast<const float4*>(tls + 8 * g + 4 * h);
+                        lse_r[4 * g] = v.x; lse_r[4 * g + 1] = v.y; lse_r[4 * g + 2] = v.z; lse_r[4 * g + 3] = v.w;
+                    }
+                }
+                float ds[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int tr = tile_row(r, h);
+                    const int64_t srow = sub0 + tr;
+                    const float l = (PASS == ROW) ? lse_f : lse_r[r];
+                    float e = exp2f(acc[r] * a.c2 - l);
+                    // label: ROW → stream item srow == user f + off; COL → item f == user srow + off
+                    const bool lab = (PASS == ROW) ? (srow == f + a.off) : (f == srow + a.off);
+                    if (lab) e -= 1.f;
+                    ds[r] = (tr < left && fok) ? e * Split<T>::kScale : 0.f;
+                }
+                s16x8 bh[2], bl[2];
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    uint32_t hp[4], lp[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) Split<T>::run(ds[8 * s2 + 2 * j], ds[8 * s2 + 2 * j + 1], hp[j], lp[j]);
+                    bh[s2] = __builtin_bit_cast(s16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
+                    bl[s2] = __builtin_bit_cast(s16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
+                }
+                // ---- gradient: gaccᵀ[d][f] += Σ_rows X[row][d] · dS[row][f] ----
+                // A = Xᵀ fragment by transposed reads: element j of half h = row 16·s2 + 8(j>>2) + 4h + (j&3)
+                const int g16 = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+#pragma unroll
+                for (int dbi = 0; dbi < G::DB; ++dbi) {
+                    const int db = db0 + dbi;
+                    const int half = db >> 2;
+                    const int c0 = ((db & 3) * 32 + 16 * (g16 & 1)) >> 3;  // chunk of the group's 16 columns
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const int r0 = rt * 32 + 16 * s2 + 4 * h;
+                        const s16x4 lo4 = tr_read(tl, img_off(half, r0 + q, c0 + (p >> 1)) + 8 * (p & 1));
+                        const s16x4 hi4 = tr_read(tl, img_off(half, r0 + 8 + q, c0 + (p >> 1)) + 8 * (p & 1));
+                        const s16x8 af = s16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+                        gacc[dbi] = MM::run(af, bh[s2], gacc[dbi]);
+                        gacc[dbi] = MM::run(af, bl[s2], gacc[dbi]);
+                    }
+                }
+            }
+        }
+        raw_barrier();
+        cur ^= 1;
+    }
+
+    if constexpr (PASS == LSE) {
+        // merge the two lane halves (same fixed row), write the split's partial
+        const float om = __shfl_xor(run_m, 32, 64), os = __shfl_xor(run_s, 32, 64);
+        const float mn = fmaxf(run_m, om);
+        float s = 0.f;
+        if (mn != -INFINITY) s = run_s * exp2f(run_m - mn) + os * exp2f(om - mn);
+        const float dgo = __shfl_xor(dg, 32, 64);
+        if (fok && h == 0) {
+            a.part[static_cast<int64_t>(split) * a.n_fixed + f] = make_float2(mn, s);
+            const int64_t lab = f + a.off;
+            if (lab >= i_begin && lab < i_end) {
+                const int64_t rr = lab - (i_begin + ((lab - i_begin) & ~31ll));
+                a.diag2[f] = ((rr >> 2) & 1) ? dgo : dg;
+            }
+        }
+    } else {
+        // gaccᵀ[db][r] = grad[d = 32db + tile_row(r,h)][fixed row f] → partial [split][f][DP]
+        if (fok) {
+            const float gs = a.inv_tau * a.w / Split<T>::kScale;
+            float* gp = a.gpart + (static_cast<int64_t>(split) * a.n_fixed + f) * DP;
+#pragma unroll
+            for (int dbi = 0; dbi < G::DB; ++dbi)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    *reinterpret_cast<float4*>(gp + 32 * (db0 + dbi) + 8 * g + 4 * h) =
+                        make_float4(gacc[dbi][4 * g] * gs, gacc[dbi][4 * g + 1] * gs, gacc[dbi][4 * g + 2] * gs,
+                                    gacc[dbi][4 * g + 3] * gs);
+        }
+    }
+}
+
+// lse2_i = log2 Σ_splits sum·2^max ; L += w_loss · mean_i (lse2_i − x_ii)/log2e
+__global__ __launch_bounds__(256) void ib16_finalize_kernel(const float2* __restrict__ part, int splits, int64_t b,
+                                                            const float* __restrict__ diag2, float* __restrict__ lse2,
+                                                            double* __restrict__ loss_out) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    double ce = 0.0;
+    if (i < b) {
+        float m = -INFINITY;
+        for (int s = 0; s < splits; ++s) m = fmaxf(m, part[static_cast<int64_t>(s) * b + i].x);
+        float sum = 0.f;
+        for (int s = 0; s < splits; ++s) {
+            const float2 v = part[static_cast<int64_t>(s) * b + i];
+            if (v.x != -INFINITY) sum += v.y * exp2f(v.x - m);
+        }
+        const float l2 = m + log2f(sum);
+        lse2[i] = l2;
+        ce = static_cast<double>((l2 - diag2[i]) / kLog2e);
+    }
+    ce = wave_sum(ce);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ce;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t = (red[0] + red[1] + red[2] + red[3]) / static_cast<double>(b);
+        atomicAdd(&loss_out[0], t);
+        atomicAdd(&loss_out[2], t);
+    }
+}
+
+// out[r][c] = Σ_s part[s][r][c] (fixed order), for c < d (part rows are DP wide)
+__global__ __launch_bounds__(256) void ib16_reduce_kernel(const float* __restrict__ part, int splits, int64_t rows,
+                                                          int dp, int d, float* __restrict__ out) {
+    const int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
+    const int64_t total = rows * d;
+    if (e >= total) return;
+    const int64_t r = e / d;
+    const int c = static_cast<int>(e - r * d);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < splits; ++s) {
+        const float4 v = *reinterpret_cast<const float4*>(part + (static_cast<int64_t>(s) * rows + r) * dp + c);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + e) = acc;
+}
+
+inline int splits_for(int64_t fixed_blocks, int64_t n_stream) {
+    int64_t s = (256 + fixed_blocks - 1) / fixed_blocks;  // ~1 block (8 waves) per CU
+    const int64_t mx = (n_stream + 4 * NT - 1) / (4 * NT);  // >= 4 stages per split
+    if (s > mx) s = mx;
+    if (s > 64) s = 64;
+    return static_cast<int>(s < 1 ? 1 : s);
+}
+
+struct PassPlan {
+    int64_t fixed_blocks;
+    int splits;
+    int64_t per;  // streamed rows per split (multiple of NT)
+};
+
+inline PassPlan pass_plan(int64_t n_fixed, int64_t n_stream, int ft) {
+    PassPlan q{};
+    q.fixed_blocks = (n_fixed + ft - 1) / ft;
+    q.splits = splits_for(q.fixed_blocks, n_stream);
+    q.per = ((n_stream + q.splits - 1) / q.splits + NT - 1) / NT * NT;
+    q.splits = static_cast<int>((n_stream + q.per - 1) / q.per);
+    return q;
+}
+
+struct Plan {
+    int dp;
+    PassPlan lse, row, col;
+    size_t part_off, diag_off, lse_off, gp_off, bytes;
+};
+
+inline Plan make_plan(int64_t b, int64_t nx, int d) {
+    Plan p{};
+    p.dp = d <= 128 ? 128 : 256;
+    const int ft_l = 256, ft_g = p.dp <= 128 ? 256 : 128;  // Geo<DP, PASS>::FT
+    p.lse = pass_plan(b, nx, ft_l);
+    p.row = pass_plan(b, nx, ft_g);
+    p.col = pass_plan(nx, b, ft_g);
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    size_t o = 0;
+    p.part_off = o; o += al(static_cast<size_t>(p.lse.splits) * b * sizeof(float2));
+    p.diag_off = o; o += al(static_cast<size_t>(b) * sizeof(float));
+    p.lse_off = o; o += al(static_cast<size_t>((b + 63) / 64 * 64 + 64) * sizeof(float));  // DMA-padded
+    p.gp_off = o;
+    const size_t g_row = static_cast<size_t>(p.row.splits) * b * p.dp * sizeof(float);
+    const size_t g_col = static_cast<size_t>(p.col.splits) * nx * p.dp * sizeof(float);
+    o += al(g_row > g_col ? g_row : g_col);
+    p.bytes = o;
+    return p;
+}
+
+}  // namespace ib16
+
+// workspace for the 16-bit in-batch path (rt_inbatch_loss_fwd_bwd, n_neg = 0)
+size_t ib16_workspace_bytes(int64_t b, int64_t nx, int d) { return ib16::make_plan(b, nx, d).bytes; }
+
+template <typename T, int DP>
+static int ib16_run_t(const void* u, const void* p, int64_t b, int64_t nx, int d, int64_t off, float inv_tau,
+                      double* loss_out, float* du, float* dp, char* ws, const ib16::Plan& pl, hipStream_t st) {
+    using namespace ib16;
+    Args a{};
+    a.d = d;
+    a.off = off;
+    a.c2 = inv_tau * kLog2e;
+    a.inv_tau = inv_tau;
+    a.w = 1.f / static_cast<float>(b);
+    a.part = reinterpret_cast<float2*>(ws + pl.part_off);
+    a.diag2 = reinterpret_cast<float*>(ws + pl.diag_off);
+    float* lse2 = reinterpret_cast<float*>(ws + pl.lse_off);
+    a.lse2 = lse2;
+    a.gpart = reinterpret_cast<float*>(ws + pl.gp_off);
+    const dim3 blk_l(Geo<DP, LSE>::WAVES * 64), blk_r(Geo<DP, ROW>::WAVES * 64), blk_c(Geo<DP, COL>::WAVES * 64);
+    auto grid = [](const PassPlan& q) { return dim3(static_cast<unsigned>(q.fixed_blocks * q.splits)); };
+    // lse
+    a.fixed = u; a.stream = p; a.n_fixed = b; a.n_stream = nx;
+    a.splits = pl.lse.splits; a.per_split = pl.lse.per;
+    hipLaunchKernelGGL((ib16_kernel<T, DP, LSE>), grid(pl.lse), blk_l, 0, st, a);
+    int rc = check_launch("ib16_kernel<lse>");
+    if (rc) return rc;
+    hipLaunchKernelGGL(ib16_finalize_kernel, dim3(static_cast<unsigned>((b + 255) / 256)), dim3(256), 0, st, a.part,
+                       pl.lse.splits, b, a.diag2, lse2, loss_out);
+    if ((rc = check_launch("ib16_finalize_kernel"))) return rc;
+    if (!du) return RT_OK;
+    // row pass: dU
+    a.splits = pl.row.splits; a.per_split = pl.row.per;
+    hipLaunchKernelGGL((ib16_kernel<T, DP, ROW>), grid(pl.row), blk_r, 0, st, a);
+    if ((rc = check_launch("ib16_kernel<row>"))) return rc;
+    hipLaunchKernelGGL(ib16_reduce_kernel, dim3(static_cast<unsigned>((b * d / 4 + 255) / 256)), dim3(256), 0, st,
+                       a.gpart, pl.row.splits, b, DP, d, du);
+    if ((rc = check_launch("ib16_reduce_kernel(du)"))) return rc;
+    // column pass: dP (items fixed, users streamed)
+    a.fixed = p; a.stream = u; a.n_fixed = nx; a.n_stream = b;
+    a.splits = pl.col.splits; a.per_split = pl.col.per;
+    hipLaunchKernelGGL((ib16_kernel<T, DP, COL>), grid(pl.col), blk_c, 0, st, a);
+    if ((rc = check_launch("ib16_kernel<col>"))) return rc;
+    hipLaunchKernelGGL(ib16_reduce_kernel, dim3(static_cast<unsigned>((nx * d / 4 + 255) / 256)), dim3(256), 0, st,
+                       a.gpart, pl.col.splits, nx, DP, d, dp);
+    return check_launch("ib16_reduce_kernel(dp)");
+}
+
+// 16-bit in-batch CE (n_neg = 0). d % 8 == 0, d <= 256; 16-B aligned rows.
+int ib16_run(const void* u, const void* p, int dtype, int64_t b, int64_t nx, int d, int64_t off, float inv_tau,
+             double* loss_out, float* du, float* dp, void* ws, size_t ws_bytes, hipStream_t st) {
+    const ib16::Plan pl = ib16::make_plan(b, nx, d);
+    if (!ws || ws_bytes < pl.bytes) return RT_ERR_WORKSPACE;
+    char* w = reinterpret_cast<char*>(ws);
+    if (dtype == RT_BF16) {
+        return pl.dp == 128 ? ib16_run_t<__hip_bfloat16, 128>(u, p, b, nx, d, off, inv_tau, loss_out, du, dp, w, pl, st)
+                            : ib16_run_t<__hip_bfloat16, 256>(u, p, b, nx, d, off, inv_tau, loss_out, du, dp, w, pl, st);
+    }
+    return pl.dp == 128 ? ib16_run_t<__half, 128>(u, p, b, nx, d, off, inv_tau, loss_out, du, dp, w, pl, st)
+                        : ib16_run_t<__half, 256>(u, p, b, nx, d, off, inv_tau, loss_out, du, dp, w, pl, st);
+}
+
+}  // namespace rt

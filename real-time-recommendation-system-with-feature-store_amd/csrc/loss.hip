@@ -27,6 +27,9 @@
 #include "rt_common.h"
 
 namespace rt {
+size_t ib16_workspace_bytes(int64_t b, int64_t nx, int d);
+int ib16_run(const void* u, const void* p, int dtype, int64_t b, int64_t nx, int d, int64_t off, float inv_tau,
+             double* loss_out, float* du, float* dp, void* ws, size_t ws_bytes, hipStream_t st);
 namespace loss {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -547,14 +550,24 @@ extern "C" size_t rt_twotower_loss_workspace_bytes(int64_t b, int d) {
 }
 
 extern "C" size_t rt_inbatch_loss_workspace_bytes(int64_t b, int64_t n_items, int d) {
-    (void)d;
-    if (b <= 0 || n_items < b) return 256;
-    return loss_ws_bytes(b, n_items) + 256;
+    if (b <= 0 || n_items < b || d <= 0) return 256;
+    // the dtype is not part of the query: room for the fp32 path and the 16-bit MFMA path
+    const size_t f32 = loss_ws_bytes(b, n_items), h16 = ib16_workspace_bytes(b, n_items, d);
+    return (f32 > h16 ? f32 : h16) + 256;
 }
 
 extern "C" int rt_inbatch_loss_fwd_bwd(const void* u, const void* p, int dtype, int64_t b, int64_t n_items, int d,
                                        int64_t label_offset, float inv_tau, double* loss_out, float* du, float* dp,
                                        void* workspace, size_t workspace_bytes, void* stream) {
+    if (dtype == RT_F16 || dtype == RT_BF16) {  // scores and gradients on the 16-bit MFMA (inbatch16.hip)
+        if (b <= 0 || d <= 0 || !u || !p || !loss_out) return RT_ERR_INVALID;
+        if (n_items < b || label_offset < 0 || label_offset + b > n_items) return RT_ERR_INVALID;
+        if (d % 8 != 0 || d > loss::kMaxD) return RT_ERR_UNSUPPORTED;
+        if ((du == nullptr) != (dp == nullptr)) return RT_ERR_INVALID;
+        if ((reinterpret_cast<uintptr_t>(u) | reinterpret_cast<uintptr_t>(p)) & 15) return RT_ERR_INVALID;
+        return ib16_run(u, p, dtype, b, n_items, d, label_offset, inv_tau, loss_out, du, dp, workspace,
+                        workspace_bytes, as_stream(stream));
+    }
     return run_loss(u, p, nullptr, dtype, b, n_items, label_offset, d, 0, inv_tau, nullptr, nullptr, 0.f, 1.f,
                     loss_out, du, dp, nullptr, nullptr, nullptr, workspace, workspace_bytes, stream, du != nullptr);
 }
