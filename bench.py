@@ -16,8 +16,10 @@ replicas on their own batches with one RCCL all-reduce of the flat grad slab
 Extras on the same line (rank 0): Flat-IP top-K QPS at config 3 (6,040 users x
 3,416 items, fp32, k=10) and a config-4 shard (65,536 queries x 125,000
 items, fp16, k=100), the HBM row-gather rate (config-5 table shard, bf16
-rows of 256), the live roofline of the dominant kernel, and the CPU baseline
-(the oracle's torch-CPU restatement of the same step on this host's cores).
+rows of 256), the config-5 in-batch scoring CE (8,192 x 8,192 x 256 bf16,
+forward and forward+backward on the 16-bit MFMA), the live roofline of the
+dominant kernel, and the CPU baseline (the oracle's torch-CPU restatement of
+the same step on this host's cores).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -162,6 +164,24 @@ def topk_extras(dev):
     out["gather_c5"] = {"GBps": gbs, "hbm_frac": gbs / PEAK_HBM_GBS, "ms": s["avg_ms"], "ids": ids.numel(),
                         "row_bytes": 512}
     del table, ids, outb
+    torch.cuda.empty_cache()
+    # config 5 in-batch scoring: S = U·Pᵀ/τ over B=8192 users x 8192 items, D=256
+    # bf16, CE forward + backward on the 16-bit MFMA path (rt_inbatch_loss_fwd_bwd)
+    u = (torch.randn(8192, 256, device=dev, generator=g) * 0.06).to(torch.bfloat16)
+    p = (torch.randn(8192, 256, device=dev, generator=g) * 0.06).to(torch.bfloat16)
+    for grad in (False, True):
+        kernels.inbatch_loss(u, p, 0.05, grad=grad)
+        torch.cuda.synchronize()
+        TIMER.enable(["inbatch_loss"])
+        for _ in range(10):
+            kernels.inbatch_loss(u, p, 0.05, grad=grad)
+        s = TIMER.summary()["inbatch_loss"]
+        TIMER.disable()
+        tf = s["flops"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e12
+        out["inbatch_c5_" + ("fwd_bwd" if grad else "fwd")] = {
+            "ms": s["avg_ms"], "tflops": tf, "mfma_frac": tf / PEAK_BF16_TFLOPS, "dtype": "bf16",
+            "shape": "8192x8192x256", "flops": "algorithmic: 2BND fwd, 6BND fwd+bwd"}
+    del u, p
     torch.cuda.empty_cache()
     return out
 

@@ -4,14 +4,18 @@
 // MovieLensDataset.__getitem__ (src/training/datasets/movielens.py:108-116) and
 // the nn.Embedding lookup (src/models/two_tower.py:115-119, 257-261): rows are
 // copied as 16-byte vectors, lanes flattened over (row, 16-B chunk) so a wave
-// covers whole rows with contiguous 1 KiB accesses, several chunks in flight
-// per lane before the stores (memory-level parallelism for the HBM roofline).
+// covers whole rows with contiguous 1 KiB accesses, one vector per thread over
+// a grid that covers the whole gather (memory-level parallelism for the HBM
+// roofline), nontemporal loads and stores.
 #include "rt_common.h"
 
 namespace rt {
 namespace gather {
 
-constexpr int kUnroll = 4;
+// one 16-B vector per thread and a grid covering every vector: the most
+// independent row reads in flight chip-wide (probe, C5 shard shape: 5.1 TB/s
+// at 4 per thread over 65,536 blocks -> 5.95 TB/s, tools/hip_probe/gather_probe.hip)
+constexpr int kUnroll = 1;
 
 // element vectors as clang ext_vector types (the nontemporal builtins need them)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -113,9 +117,8 @@ using namespace rt;
 template <typename V>
 static void launch_gather(const void* table, int64_t row_begin, int64_t n_rows, uint32_t vpr, const int64_t* ids,
                           int64_t n_ids, void* out, int32_t* oob, hipStream_t st) {
-    // large grids keep more independent row reads in flight across the chip
-    // (probe: 4096 -> 65536 blocks raised a float4 copy from 4.6 to 5.3 TB/s)
-    const unsigned grid = gather::grid_for(n_ids * vpr / gather::kUnroll, 256, 65536);
+    // a grid over every vector keeps the most independent row reads in flight
+    const unsigned grid = gather::grid_for(n_ids * vpr / gather::kUnroll, 256, 0x7FFFFFFF);
     if (n_ids * static_cast<int64_t>(vpr) + static_cast<int64_t>(grid) * 256 * gather::kUnroll < (1ll << 32)) {
         hipLaunchKernelGGL((gather::gather_rows_kernel<V, uint32_t>), dim3(grid), dim3(256), 0, st,
                            reinterpret_cast<const V*>(table), row_begin, n_rows, vpr, ids, n_ids,
