@@ -277,6 +277,17 @@ def main():
         achieved = per_launch_bytes / avg_s / 1e9
         roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None}
+    # HBM traffic per launch of the dominant kernel: rocprofv3 FETCH_SIZE / WRITE_SIZE
+    # passes of this same bench command (profiles/r01_traffic.json, tools/traffic_json.py)
+    tpath = os.path.join(REPO, "profiles", "r01_traffic.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        tb = tj.get("bytes_per_launch", {}).get(dominant)
+        if tb is not None:
+            roof["traffic"] = float(tb)
+            roof["traffic_unit"] = "bytes/launch (PMC)"
+            roof["traffic_source"] = "profiles/r01_traffic.json: " + tj.get("correction", "")
     roof.update({"kernel": dominant, "launches_per_step": d["count"] / args.steps,
                  "measured": ("HIP events around each launch over an eager replay of the timed steps"
                               if args.graph else "HIP events around each launch inside the timed region"),

@@ -12,9 +12,21 @@ import sys
 from collections import defaultdict
 
 
-def from_db(path):
+def from_db(path, by_grid=False, by_base=False):
     c = sqlite3.connect(path)
-    rows = c.execute("select name, duration from kernels").fetchall()
+    cols = [d[0] for d in c.execute("select * from kernels limit 1").description]
+    gcols = [g for g in cols if "grid" in g.lower()] if by_grid else []
+    q = "select name, duration" + "".join(f", {g}" for g in gcols) + " from kernels"
+    rows = []
+    for r in c.execute(q).fetchall():
+        name = r[0]
+        if by_grid or by_base:
+            name = name.split("(")[0]
+        if by_base:
+            name = name.split("<")[0].replace("void ", "")
+        if gcols:
+            name += " " + " ".join(f"{g}={v}" for g, v in zip(gcols, r[2:]))
+        rows.append((name, r[1]))
     return rows
 
 
@@ -45,7 +57,7 @@ def main():
     ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size) = per launch shape")
     ap.add_argument("--by-base", action="store_true", help="one row per kernel family (all template instances)")
     a = ap.parse_args()
-    rows = from_db(a.src) if a.src.endswith(".db") else from_csv(a.src, a.by_grid, a.by_base)
+    rows = from_db(a.src, a.by_grid, a.by_base) if a.src.endswith(".db") else from_csv(a.src, a.by_grid, a.by_base)
     agg = defaultdict(list)
     for name, dur in rows:
         agg[name].append(dur)
