@@ -305,11 +305,12 @@ namespace rt {
 namespace topk {
 
 // kernel choice: register lists (this file) for fp32 with k <= 32; the
-// radix-compacted candidate-buffer kernel (topk_v2.h) for 16-bit with
-// k <= 128; the sorted candidate-buffer kernel (topk_v1.h) otherwise.
+// radix-compacted candidate-buffer kernel (topk_v2.h) for every dtype with
+// k <= 128 otherwise; the sorted candidate-buffer kernel (topk_v1.h) above.
 // Returns K for the list kernel, 0 for v1, -2 for v2.
 inline int list_k(bool f32, int k) {
-    if (f32) return k <= 16 ? 16 : k <= 32 ? 32 : 0;
+    if (f32 && k <= 16) return 16;  // small fp32 queries: per-lane register lists (C3, serving)
+    if (f32 && k <= 32) return 32;
     return k <= v2::kMaxKv2 ? -2 : 0;
 }
 
@@ -322,9 +323,8 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
             case 32: return launch_cfg<T, S, 32>(a, p, st);
             default: break;
         }
-    } else {
-        if (list_k(false, a.k) == -2) return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
     }
+    if (list_k(F32, a.k) == -2) return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
     return v1::launch_S<T, S>(a, p.cap, p.splits, p.items_per_split, st);
 }
 

@@ -201,12 +201,12 @@ __device__ __forceinline__ void wait_vm_le(int n) {
 
 template <typename T, int S>
 struct Cfg2 {
-    static constexpr int KK = Mfma<T>::kK;                      // 16
+    static constexpr int KK = Mfma<T>::kK;                      // k per MFMA: 16 (f16/bf16), 2 (f32)
     static constexpr int DP = S * KK;                            // padded d
     static constexpr int VEC = 16 / static_cast<int>(sizeof(T));  // 8 elements per 16 B
     static constexpr int ROWB = DP * static_cast<int>(sizeof(T));   // bytes per LDS row (unpadded)
     static constexpr int P = ROWB / 16;                              // 16-byte chunks per row
-    static constexpr int NT = S <= 8 ? 128 : 64;                    // items per LDS stage
+    static constexpr int NT = ROWB <= 256 ? 128 : 64;               // items per LDS stage
     static constexpr int TILE_BYTES = NT * ROWB;
     static constexpr int DMA_PER_WAVE = TILE_BYTES / 1024 / kWavesB;  // 1 KiB per wave-instruction
     static_assert(DMA_PER_WAVE * 1024 * kWavesB == TILE_BYTES, "tile must split into whole DMA pieces");
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
         const T* qrow = Q + (qok ? q : 0) * d;
 #pragma unroll
         for (int s = 0; s < S; ++s) {
-            const int k0 = 16 * s + 8 * half;
+            const int k0 = (C::KK == 2) ? 2 * s + half : 16 * s + 8 * half;
             if (qok && k0 < d) qf[s] = frag_from<T>(qrow + k0);
             else qf[s] = typename M::frag{};
         }
@@ -274,8 +274,12 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     // wait state would force a vmcnt(0) (and so the tile prefetch) every tile
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-        const uint4 t = __builtin_bit_cast(uint4, qf[s]);
-        asm volatile("" ::"v"(t.x), "v"(t.y), "v"(t.z), "v"(t.w));
+        if constexpr (C::KK == 2) {
+            asm volatile("" ::"v"(qf[s]));
+        } else {
+            const uint4 t = __builtin_bit_cast(uint4, qf[s]);
+            asm volatile("" ::"v"(t.x), "v"(t.y), "v"(t.z), "v"(t.w));
+        }
     }
     const uint32_t* excl = (EXCL && qok) ? a.excl + q * a.excl_words : nullptr;
     float thr = qok ? -FLT_MAX : INFINITY;
@@ -392,11 +396,22 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
             f32x16 acc = {};
             const int row = rt * 32 + col;
             const T* arow = tl + row * DP;
-            typename M::frag af[S];
+            if constexpr (C::KK == 2) {
+                // f32: k-step s takes element 2s + half (natural k order: the MFMA chain
+                // is the oracle's sequential fmaf order); one b128 read serves 2 steps
 #pragma unroll
-            for (int s = 0; s < S; ++s) af[s] = frag_from<T>(arow + ((2 * s + half) ^ C::swz(row)) * VEC);
+                for (int j = 0; j < S / 2; ++j) {
+                    const float4 v = *reinterpret_cast<const float4*>(arow + (j ^ C::swz(row)) * VEC);
+                    acc = M::run(half ? v.y : v.x, qf[2 * j], acc);
+                    acc = M::run(half ? v.w : v.z, qf[2 * j + 1], acc);
+                }
+            } else {
+                typename M::frag af[S];
 #pragma unroll
-            for (int s = 0; s < S; ++s) acc = M::run(af[s], qf[s], acc);
+                for (int s = 0; s < S; ++s) af[s] = frag_from<T>(arow + ((2 * s + half) ^ C::swz(row)) * VEC);
+#pragma unroll
+                for (int s = 0; s < S; ++s) acc = M::run(af[s], qf[s], acc);
+            }
             if (sub0 + 32 > i_end) {  // rows past the end never qualify
                 const int left = static_cast<int>(i_end - sub0);
 #pragma unroll
@@ -432,9 +447,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
 }
 
 inline int planned_splits(int64_t q_tiles, int64_t nx) {
-    // ~1 block (8 waves) per CU; keep every split >= 16 LDS stages
+    // ~1 block (8 waves) per CU (fewer splits = fewer early-phase appends);
+    // every split >= 2 LDS stages, so small corpora still fill the chip
     int64_t splits = (256 + q_tiles - 1) / q_tiles;
-    int64_t max_splits = (nx + 16 * kNT - 1) / (16 * kNT);
+    int64_t max_splits = (nx + 2 * kNT - 1) / (2 * kNT);
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
     // powers of two up to 8 keep one split per XCD
