@@ -186,6 +186,51 @@ def topk_extras(dev):
     return out
 
 
+def topk_c4_scaling(dev, dist, rank, world, reps=3):
+    """C4 scaling leg, run collectively on every rank: a 1M-item f16 corpus
+    (emb 128) row-sharded over the ranks (1M/N rows each), 65,536 queries per
+    launch scanned by every rank against its shard (k=100), the per-slice
+    candidate lists sent to the query owners by one all-to-all, owner merge
+    (src/dist/sharded.py::sharded_topk_owner). Strong scaling (fixed corpus);
+    time = max over ranks between barriers."""
+    from src import kernels
+    from src.dist.sharded import shard_range, sharded_topk_owner
+    n, d, nq, k = 1_000_000, 128, 65536, 100
+    b, c = shard_range(n, world, rank)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    shard = torch.nn.functional.normalize(torch.randn(c, d, device=dev, generator=g), dim=1).half()
+    gq = torch.Generator(device=dev).manual_seed(99)
+    q = torch.nn.functional.normalize(torch.randn(nq, d, device=dev, generator=gq), dim=1).half()
+    grp = dist.group.WORLD if dist is not None else None
+
+    def run():
+        return sharded_topk_owner(q, k, lambda qq, kk: kernels.flatip_topk(qq, shard, kk, id_offset=b),
+                                  kernels.topk_merge, grp)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    run()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    del shard, q
+    torch.cuda.empty_cache()
+    return {"qps": nq * reps / el, "ms_per_launch": 1e3 * el / reps, "n_gpus": world, "corpus_rows": n,
+            "shard_rows": c, "queries_per_launch": nq, "k": k, "dtype": "f16", "exchange": "all_to_all + owner merge",
+            "scaling": "strong (fixed 1M-row corpus)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,6 +352,12 @@ def main():
                    "parallelism": f"dp{world}", "final_loss": final_loss},
         "roofline": roof,
     }
+    scaling = None
+    if not args.no_extras:  # collective: every rank
+        try:
+            scaling = topk_c4_scaling(dev, dist, rank, world)
+        except Exception as e:  # extras never hide the headline
+            scaling = {"error": repr(e)}
     if rank == 0 and world == 1:
         if not args.no_extras:
             try:
@@ -315,6 +366,8 @@ def main():
                 result["extras"] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(host, args.cpu_budget)
+    if scaling is not None:
+        result.setdefault("extras", {})["topk_c4_1m_sharded"] = scaling
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

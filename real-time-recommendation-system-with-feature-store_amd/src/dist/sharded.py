@@ -95,6 +95,32 @@ def sharded_topk(queries: torch.Tensor, k: int, local_topk: TopkFn, merge: Merge
     return merge(all_s, all_i, k)
 
 
+def sharded_topk_owner(queries: torch.Tensor, k: int, local_topk: TopkFn, merge: MergeFn,
+                       group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact top-k over a row-sharded corpus where each rank OWNS a contiguous
+    slice of the queries (``shard_range(nq, world, rank)``): every rank scans
+    all queries against its shard, one ``all_to_all_single`` sends each query
+    slice's (score, id) lists to its owner, and the owner merges world lists
+    per query. Per-rank exchange volume is nq·k·12 B (an all-gather would move
+    world× that to every rank), so the step stays scan-bound as world grows.
+    Returns this rank's slice [nq_own, k]. nq must split evenly (nq % world == 0)."""
+    s, i = local_topk(queries, k)
+    world, rank = _world(group)
+    if world == 1:
+        return s, i
+    nq = s.shape[0]
+    if nq % world:
+        raise ValueError(f"{nq} queries do not split over {world} ranks")
+    s = s.contiguous()
+    i = i.contiguous()
+    out_s = torch.empty_like(s)
+    out_i = torch.empty_like(i)
+    dist.all_to_all_single(out_s, s, group=group)
+    dist.all_to_all_single(out_i, i, group=group)
+    per = nq // world
+    return merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
+
+
 def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Tensor, group=None,
                         gather: Optional[Callable] = None) -> torch.Tensor:
     """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL

@@ -20,7 +20,7 @@ import torch.multiprocessing as mp
 
 from oracle import flat_ip as orc
 from src.dist.sharded import (allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_inbatch_step,
-                               sharded_topk)
+                               sharded_topk, sharded_topk_owner)
 
 
 def _free_port():
@@ -96,6 +96,35 @@ def _topk_worker(rank, world, n, d, nq, k, seed, with_ties):
 @pytest.mark.parametrize("n,k,ties", [(1001, 10, False), (300, 100, True), (37, 50, False)])
 def test_sharded_topk_matches_single_index_gloo(n, k, ties):
     _run(2, _topk_worker, n, 32, 19, k, 7, ties)
+
+
+def _topk_owner_worker(rank, world, n, d, nq, k, seed):
+    rng = np.random.default_rng(seed)
+    corpus = _dyadic(rng, n, d)
+    corpus[n - 1] = corpus[0]  # a tie across the shard boundary
+    queries = _dyadic(rng, nq, d)
+    b, c = shard_range(n, world, rank)
+
+    def local(q, kk):
+        s, i = orc.flat_ip_search(q.numpy(), corpus[b:b + c], kk, id_offset=b)
+        return torch.from_numpy(s), torch.from_numpy(i)
+
+    def merge(s, i, kk):
+        ms, mi = orc.topk_merge(s.numpy(), i.numpy(), kk)
+        return torch.from_numpy(ms), torch.from_numpy(mi)
+
+    got_s, got_i = sharded_topk_owner(torch.from_numpy(queries), k, local, merge)
+    qb, qc = shard_range(nq, world, rank)
+    ref_s, ref_i = orc.flat_ip_search(queries[qb:qb + qc], corpus, k)
+    np.testing.assert_array_equal(got_i.numpy(), ref_i)
+    np.testing.assert_array_equal(got_s.numpy(), ref_s)
+
+
+@pytest.mark.parametrize("world,n,k", [(2, 1001, 10), (4, 500, 100)])
+def test_sharded_topk_query_owner_gloo(world, n, k):
+    """C4 at N GPUs: all-to-all of per-slice candidate lists, the query owner
+    merges — equal to one index over the whole corpus for the owned queries."""
+    _run(world, _topk_owner_worker, n, 32, 24, k, 11)
 
 
 def _gather_worker(rank, world, n, d, seed):
