@@ -48,6 +48,26 @@ __device__ __forceinline__ float pro_apply(const Pro& p, int64_t r, int c, float
     return v;
 }
 
+// (Σ slot[c], Σ slot[w + c]) over the RT_STAT_SLOTS fp64 slots of stride 2w, in
+// slot order: all 2·RT_STAT_SLOTS loads are issued before the first add (one
+// memory round trip instead of a dependent chain — the slots are written by
+// memory-side atomics, so every load is an HBM/MALL latency)
+__device__ __forceinline__ void slot_sums(const double* __restrict__ base, int w, int c, double& s1, double& s2) {
+    double v1[RT_STAT_SLOTS], v2[RT_STAT_SLOTS];
+#pragma unroll
+    for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+        v1[sl] = base[static_cast<int64_t>(sl) * 2 * w + c];
+        v2[sl] = base[static_cast<int64_t>(sl) * 2 * w + w + c];
+    }
+    s1 = 0.0;
+    s2 = 0.0;
+#pragma unroll
+    for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+        s1 += v1[sl];
+        s2 += v2[sl];
+    }
+}
+
 __device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, float invstd, float& scale,
                                           float& shift) {
     scale = gamma * invstd;
@@ -96,12 +116,8 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
                 float mean, invstd, var_f = 0.f;
                 if (a.prev_mode == 1) {
                     const double* ps = a.prev_stats + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * k;
-                    double s1 = 0.0, s2 = 0.0;  // slot sums in slot order
-#pragma unroll 4
-                    for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
-                        s1 += ps[static_cast<int64_t>(sl) * 2 * k + c];
-                        s2 += ps[static_cast<int64_t>(sl) * 2 * k + k + c];
-                    }
+                    double s1, s2;  // slot sums in slot order
+                    slot_sums(ps, k, c, s1, s2);
                     const double md = s1 / static_cast<double>(ms);
                     double vd = s2 / static_cast<double>(ms) - md * md;
                     vd = vd > 0.0 ? vd : 0.0;
@@ -363,12 +379,8 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
                 M = a.save_mean[my_seg * n + c];
                 A = a.bn_gamma[c] * I;
                 if (a.grad_mode == 1) {
-                    double gs1 = 0.0, gs2 = 0.0;
-#pragma unroll 4
-                    for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
-                        gs1 += gst[static_cast<int64_t>(sl) * 2 * n + c];
-                        gs2 += gst[static_cast<int64_t>(sl) * 2 * n + n + c];
-                    }
+                    double gs1, gs2;
+                    slot_sums(gst, n, c, gs1, gs2);
                     Bc = static_cast<float>(gs1) * inv_m;
                     C = static_cast<float>(gs2) * inv_m;
                 }
@@ -438,11 +450,8 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
         for (int c = tid; c < n; c += 256) {
             for (int sg = 0; sg < (two ? 2 : 1); ++sg) {
                 const double* gs = a.g_stats + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * n;
-                double gs1 = 0.0, gs2 = 0.0;
-                for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
-                    gs1 += gs[static_cast<int64_t>(sl) * 2 * n + c];
-                    gs2 += gs[static_cast<int64_t>(sl) * 2 * n + n + c];
-                }
+                double gs1, gs2;
+                slot_sums(gs, n, c, gs1, gs2);
                 atomicAdd(&a.dgamma[c], static_cast<float>(gs2));  // atomic: concurrent chains of one tower
                 atomicAdd(&a.dbeta[c], static_cast<float>(gs1));
             }
