@@ -233,17 +233,22 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             const int left = static_cast<int>(i_end - sub0 < 32 ? i_end - sub0 : 32);
             if constexpr (PASS == LSE) {
                 float x[16];
-                float mx = -INFINITY;
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    x[r] = tile_row(r, h) < left ? acc[r] * a.c2 : -INFINITY;
-                    mx = fmaxf(mx, x[r]);
+                for (int r = 0; r < 16; ++r) x[r] = acc[r] * a.c2;
+                if (left < 32) {  // partial last sub-tile (block-uniform)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (tile_row(r, h) >= left) x[r] = -INFINITY;
                 }
-                const float mn = fmaxf(run_m, mx);
-                float s = run_s * exp2f(run_m - mn);
-                if (mn == -INFINITY) s = 0.f;
+                float mx = x[0];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) s += exp2f(x[r] - mn);
+                for (int r = 1; r < 16; ++r) mx = fmaxf(mx, x[r]);
+                const float mn = fmaxf(run_m, mx);
+                // raw v_exp_f32: arguments are <= 0, results below 2^-126 flush to 0
+                // (negligible next to the max term's 1)
+                float s = (mn == -INFINITY) ? 0.f : run_s * __builtin_amdgcn_exp2f(run_m - mn);
+#pragma unroll
+                for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(x[r] - mn);
                 run_m = mn;
                 run_s = s;
                 // label column: stream row f + off
@@ -271,11 +276,16 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
                     const int tr = tile_row(r, h);
                     const int64_t srow = sub0 + tr;
                     const float l = (PASS == ROW) ? lse_f : lse_r[r];
-                    float e = exp2f(acc[r] * a.c2 - l);
+                    float e = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
                     // label: ROW → stream item srow == user f + off; COL → item f == user srow + off
                     const bool lab = (PASS == ROW) ? (srow == f + a.off) : (f == srow + a.off);
                     if (lab) e -= 1.f;
-                    ds[r] = (tr < left && fok) ? e * Split<T>::kScale : 0.f;
+                    ds[r] = fok ? e * Split<T>::kScale : 0.f;
+                }
+                if (left < 32) {  // partial last sub-tile (block-uniform)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        if (tile_row(r, h) >= left) ds[r] = 0.f;
                 }
                 s16x8 bh[2], bl[2];
 #pragma unroll
