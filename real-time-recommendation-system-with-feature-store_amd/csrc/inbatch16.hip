@@ -22,9 +22,16 @@
 // Item/user tiles arrive by LDS-DMA into a [NT][128-col] image per 128-column
 // half whose 16-byte chunks are XOR-swizzled so that both the row reads
 // (ds_read_b128) and the transposed reads are bank-conflict free.
+// Every sub-tile issues all of its LDS fragment reads before the MFMAs that
+// consume them (at one wave per SIMD a read an MFMA waits on exposes its whole
+// latency); full stages are software-pipelined by one sub-tile (the S MFMAs of
+// sub-tile t+1 overlap the exp/split VALU work of sub-tile t) and carry no tail
+// masks or early exits.
 // Gradient partials of each split are summed by a fixed-order reduce launch
 // (deterministic, no atomics).
 #include <float.h>
+
+#include <type_traits>
 
 #include "rt_common.h"
 
@@ -32,10 +39,10 @@ namespace rt {
 namespace ib16 {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
-constexpr int NT = 64;            // streamed rows per LDS stage
 constexpr float kLog2e = 1.4426950408889634f;
 
 template <typename T> struct M16;
@@ -54,11 +61,13 @@ template <> struct M16<__half> {
     }
 };
 
-__device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+// accumulator element r of lane half h holds tile row krow(r) + 4h
+__host__ __device__ constexpr int krow(int r) { return (r & 3) + 8 * (r >> 2); }
 
 // ---- LDS image: per 128-column half, [NT rows][16 chunks of 16 B], chunk
 // index XOR-swizzled by row (conflict-free row reads AND tr_b16 reads)
 __device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+template <int NT>
 __device__ __forceinline__ int img_off(int half, int row, int ch) {
     return half * (NT * 256) + row * 256 + ((ch ^ swz(row)) << 4);
 }
@@ -76,6 +85,14 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
                  : "v"(gsrc), "s"(lds_dst)
                  : "memory");
 }
+// same, wave-uniform base + 32-bit per-lane byte offset (SADDR form: no per-lane 64-bit address math)
+__device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds_dst)
+                 : "memory");
+}
 // transposed LDS read (ds_read_b64_tr_b16): for the 16-lane group of this lane,
 // lane 4q+p addresses row q / columns 4p..4p+3 of a 4 x 16 block; lane i gets column i
 __device__ __forceinline__ s16x4 tr_read(const char* lds, int byte_off) {
@@ -83,26 +100,31 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds, int byte_off) {
         (__attribute__((address_space(3))) s16x4*)(lds + byte_off));
 }
 
-// x → (hi, lo) 16-bit pair with x ≈ hi + lo; two elements packed per dword (lo element first)
+// x → (hi, lo) 16-bit pair with x ≈ hi + lo; two elements packed per dword (lo
+// element first); one v_cvt_pk per pair and rounding, RNE
 template <typename T> struct Split;
 template <> struct Split<__hip_bfloat16> {
     static constexpr float kScale = 1.f;  // bf16 keeps the fp32 exponent range
+    static constexpr float kLog2Scale = 0.f;
     __device__ static void run(float x0, float x1, uint32_t& hp, uint32_t& lp) {
-        const __hip_bfloat16 h0 = __float2bfloat16(x0), h1 = __float2bfloat16(x1);
-        const __hip_bfloat16 l0 = __float2bfloat16(x0 - __bfloat162float(h0));
-        const __hip_bfloat16 l1 = __float2bfloat16(x1 - __bfloat162float(h1));
-        hp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
-        lp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l1)) << 16);
+        typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+        const uint32_t hv = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{x0, x1}, b2));
+        const float r0 = x0 - __builtin_bit_cast(float, hv << 16);
+        const float r1 = x1 - __builtin_bit_cast(float, hv & 0xffff0000u);
+        hp = hv;
+        lp = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{r0, r1}, b2));
     }
 };
 template <> struct Split<__half> {
     static constexpr float kScale = 32768.f;  // dS·2^15 keeps small probabilities out of f16 underflow
+    static constexpr float kLog2Scale = 15.f;
     __device__ static void run(float x0, float x1, uint32_t& hp, uint32_t& lp) {
-        const __half h0 = __float2half_rn(x0), h1 = __float2half_rn(x1);
-        const __half l0 = __float2half_rn(x0 - __half2float(h0));
-        const __half l1 = __float2half_rn(x1 - __half2float(h1));
-        hp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, h1)) << 16);
-        lp = static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l0)) | (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, l1)) << 16);
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        const h2 hv = __builtin_convertvector(f32x2{x0, x1}, h2);
+        const float r0 = x0 - static_cast<float>(hv[0]);
+        const float r1 = x1 - static_cast<float>(hv[1]);
+        hp = __builtin_bit_cast(uint32_t, hv);
+        lp = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{r0, r1}, h2));
     }
 };
 
@@ -130,9 +152,12 @@ template <int DP, int PASS> struct Geo {
     // gradient passes at DP=256 hold 8 accumulator tiles (128 registers): one
     // wave per SIMD with the 512-register file; everything else two per SIMD
     static constexpr int WAVES = (PASS != 0 && DP > 128) ? 4 : 8;
-    static constexpr int DSPLIT = 1;
-    static constexpr int DB = DP / 32 / DSPLIT;         // 32-wide d blocks per wave
-    static constexpr int FT = 32 * WAVES / DSPLIT;      // fixed rows per block
+    // streamed rows per LDS stage: 128 for the one-wave-per-SIMD gradient passes
+    // (4 sub-tiles to pipeline over), 64 where two waves per SIMD share the registers
+    static constexpr int NT = (PASS != 0 && DP > 128) ? 128 : 64;
+    static constexpr int SUB = NT / 32;                 // 32-row sub-tiles per stage
+    static constexpr int DB = DP / 32;                  // 32-wide d blocks of the gradient
+    static constexpr int FT = 32 * WAVES;               // fixed rows per block
     static constexpr int TILE_BYTES = NT * DP * 2;
     static constexpr int DMA_PER_WAVE = TILE_BYTES / 1024 / WAVES;
     static_assert(DMA_PER_WAVE * 1024 * WAVES == TILE_BYTES, "tile must split into whole DMA pieces");
@@ -142,7 +167,7 @@ template <typename T, int DP, int PASS>
 __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args a) {
     using G = Geo<DP, PASS>;
     using MM = M16<T>;
-    constexpr int S16 = G::S16;
+    constexpr int S16 = G::S16, NT = G::NT, DPW = G::DMA_PER_WAVE;
     __shared__ __attribute__((aligned(1024))) char tile[2][G::TILE_BYTES];
     __shared__ __attribute__((aligned(16))) float tlse[2][NT];  // COL: lse2 of the streamed users
 
@@ -152,9 +177,7 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 31, h = lane >> 5;
     const int split = static_cast<int>(blockIdx.x % static_cast<unsigned>(a.splits));
     const int64_t fblk = blockIdx.x / static_cast<unsigned>(a.splits);
-    const int64_t fw = fblk * G::FT + (wave / G::DSPLIT) * 32;  // wave's first fixed row
-    const int db0 = (wave % G::DSPLIT) * G::DB;                 // first d block of this wave's gradient
-    const int64_t f = fw + col;                     // this lane's fixed row (its MFMA column)
+    const int64_t f = fblk * G::FT + wave * 32 + col;  // this lane's fixed row (its MFMA column)
     const bool fok = f < a.n_fixed;
     const int64_t i_begin = static_cast<int64_t>(split) * a.per_split;
     const int64_t i_end = (i_begin + a.per_split) < a.n_stream ? (i_begin + a.per_split) : a.n_stream;
@@ -180,25 +203,46 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
 #pragma unroll
         for (int i = 0; i < G::DB; ++i) gacc[i] = f32x16{};
     }
-    if constexpr (PASS == ROW) lse_f = fok ? a.lse2[f] : 0.f;
+    // dS scale folded into the exponent; a padding lane (fixed row past the end)
+    // only feeds its own, never stored, gradient column, so it needs no mask
+    if constexpr (PASS == ROW) lse_f = (fok ? a.lse2[f] : 0.f) - Split<T>::kLog2Scale;
+    const int64_t lab_row = f + a.off;  // LSE: the item that is this user's label
 
+    // ---- LDS-DMA of one stage: 1 KiB per wave-instruction into the lane-linear image ----
     const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
-    auto fetch = [&](int64_t t0, int buf) {
-        const uint32_t base = lds_addr(&tile[buf][0]) + wave_u * (G::DMA_PER_WAVE * 1024);
+    const bool full_rows = (d == DP);  // no zero-filled columns: fixed per-lane offsets
+    uint32_t voff[DPW];                // this lane's byte offset from the stage's first row
 #pragma unroll
-        for (int j = 0; j < G::DMA_PER_WAVE; ++j) {
-            const int o = (wave * G::DMA_PER_WAVE + j) * 1024 + lane * 16;
-            const int half = o / (NT * 256);
-            const int oo = o - half * (NT * 256);
-            const int r = oo >> 8;
-            const int c = half * 16 + (((oo & 255) >> 4) ^ swz(r));  // global 16-B chunk of the row
-            int64_t item = t0 + r;
-            item = item < i_end ? item : i_end - 1;
-            const void* src = c < row_vecs ? static_cast<const void*>(X + item * d + c * 8)
-                                           : static_cast<const void*>(&kZero16);
-            glds16(src, base + j * 1024);
+    for (int j = 0; j < DPW; ++j) {
+        const int o = (wave * DPW + j) * 1024 + lane * 16;
+        const int half = o / (NT * 256);
+        const int oo = o - half * (NT * 256);
+        const int r = oo >> 8;
+        const int c = half * 16 + (((oo & 255) >> 4) ^ swz(r));
+        voff[j] = static_cast<uint32_t>(r * d * 2 + c * 16);
+    }
+    auto fetch = [&](int64_t t0, int buf) {
+        const uint32_t base = lds_addr(&tile[buf][0]) + wave_u * (DPW * 1024);
+        if (full_rows && t0 + NT <= a.n_stream) {
+            const void* sb = X + t0 * d;
+#pragma unroll
+            for (int j = 0; j < DPW; ++j) glds16_s(sb, voff[j], base + j * 1024);
+        } else {  // zero-filled columns past d and/or rows clamped at the split end
+#pragma unroll
+            for (int j = 0; j < DPW; ++j) {
+                const int o = (wave * DPW + j) * 1024 + lane * 16;
+                const int half = o / (NT * 256);
+                const int oo = o - half * (NT * 256);
+                const int r = oo >> 8;
+                const int c = half * 16 + (((oo & 255) >> 4) ^ swz(r));  // global 16-B chunk of the row
+                int64_t item = t0 + r;
+                item = item < i_end ? item : i_end - 1;
+                const void* src = c < row_vecs ? static_cast<const void*>(X + item * d + c * 8)
+                                               : static_cast<const void*>(&kZero16);
+                glds16(src, base + j * 1024);
+            }
         }
-        if constexpr (PASS == COL) {  // 64 lse2 values: 16 lanes x 16 B (the array is padded to 64)
+        if constexpr (PASS == COL) {  // NT lse2 values, 16 B per lane (the array is padded past b)
             if (wave == 0 && lane < NT / 4) glds16(a.lse2 + t0 + 4 * lane, lds_addr(&tlse[buf][0]));
         }
     };
@@ -208,117 +252,185 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
         asm volatile("" ::: "memory");
     };
 
+    // ---- pieces of one 32-row sub-tile rt of the stage image tl ----
+    auto load_s = [&](const char* tl, int rt, s16x8 (&af)[S16]) {  // A fragments of the S tile
+        const int row = rt * 32 + col;
+#pragma unroll
+        for (int s = 0; s < S16; ++s) {
+            const int cg = 2 * s + h;
+            af[s] = __builtin_bit_cast(s16x8, *reinterpret_cast<const uint4*>(tl + img_off<NT>(cg >> 4, row, cg & 15)));
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep every read issued ahead of the MFMAs
+    };
+    // S tile: acc[r] = <stream row sub0 + krow(r) + 4h, fixed row f>
+    auto mma_s = [&](const s16x8 (&af)[S16]) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int s = 0; s < S16; ++s) acc = MM::run(af[s], qf[s], acc);
+        return acc;
+    };
+    // transposed streamed-row fragments for the gradient: element j of half h = row
+    // 16·s2 + 8(j>>2) + 4h + (j&3)
+    auto load_g = [&](const char* tl, int rt, s16x8 (&ga)[G::DB][2]) {
+        const int g16 = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+#pragma unroll
+        for (int db = 0; db < G::DB; ++db) {
+            const int half = db >> 2;
+            const int c0 = ((db & 3) * 32 + 16 * (g16 & 1)) >> 3;  // chunk of the group's 16 columns
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r0 = rt * 32 + 16 * s2 + 4 * h;
+                const s16x4 lo4 = tr_read(tl, img_off<NT>(half, r0 + q, c0 + (p >> 1)) + 8 * (p & 1));
+                const s16x4 hi4 = tr_read(tl, img_off<NT>(half, r0 + 8 + q, c0 + (p >> 1)) + 8 * (p & 1));
+                ga[db][s2] = s16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+            }
+        }
+    };
+    // this lane's label row inside the sub-tile at sub0, relative to its lane half
+    auto lab_pos = [&](int64_t sub0) {
+        const int64_t dl = lab_row - sub0;
+        return (dl >= 0 && dl < 32 ? static_cast<int>(dl) : 64) - 4 * h;
+    };
+    // LSE: online base-2 log-sum-exp over the sub-tile's valid rows (left of 32)
+    auto lse_update = [&](const f32x16& acc, int64_t sub0, int left) {
+        const int lim = left - 4 * h;  // row krow(r) + 4h is valid <=> krow(r) < lim
+        float x[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) x[r] = acc[r] * a.c2;
+        if (left < 32) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (krow(r) >= lim) x[r] = -INFINITY;
+        }
+        float mx = x[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, x[r]);
+        const float mn = fmaxf(run_m, mx);
+        // raw v_exp_f32: arguments are <= 0, results below 2^-126 flush to 0
+        // (negligible next to the max term's 1)
+        float s = (mn == -INFINITY) ? 0.f : run_s * __builtin_amdgcn_exp2f(run_m - mn);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(x[r] - mn);
+        run_m = mn;
+        run_s = s;
+        const int lr = lab_pos(sub0);
+        if (fok && static_cast<unsigned>(lr) < 28u) {  // this lane holds its label's logit
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (krow(r) == lr) dg = x[r];
+        }
+    };
+    // ROW/COL: the softmax part of dS, 2^(x − lse2_user)·kScale, in registers as
+    // 16-bit hi + lo (the label term −[label] is applied by the reduce launch)
+    auto make_ds = [&](const f32x16& acc, const float* tls, int rt, int64_t sub0, int left, s16x8 (&bh)[2],
+                       s16x8 (&bl)[2]) {
+        float lse_r[16];
+        if constexpr (PASS == COL) {  // users are the streamed rows: lse2 per row, from LDS
+            const float* t = tls + rt * 32;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 v = *reinterpret_cast<const float4*>(t + 8 * g + 4 * h);
+                lse_r[4 * g] = v.x; lse_r[4 * g + 1] = v.y; lse_r[4 * g + 2] = v.z; lse_r[4 * g + 3] = v.w;
+            }
+        }
+        float ds[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float l = (PASS == ROW) ? lse_f : lse_r[r] - Split<T>::kLog2Scale;
+            ds[r] = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
+        }
+        if (left < 32) {
+            const int lim = left - 4 * h;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (krow(r) >= lim) ds[r] = 0.f;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            uint32_t hp[4], lp[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Split<T>::run(ds[8 * s2 + 2 * j], ds[8 * s2 + 2 * j + 1], hp[j], lp[j]);
+            bh[s2] = __builtin_bit_cast(s16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
+            bl[s2] = __builtin_bit_cast(s16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
+        }
+    };
+    // gradient: gaccᵀ[d][f] += Σ_rows X[row][d] · dS[row][f]
+    auto mma_g = [&](const s16x8 (&ga)[G::DB][2], const s16x8 (&bh)[2], const s16x8 (&bl)[2]) {
+#pragma unroll
+        for (int db = 0; db < G::DB; ++db)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                gacc[db] = MM::run(ga[db][s2], bh[s2], gacc[db]);
+                gacc[db] = MM::run(ga[db][s2], bl[s2], gacc[db]);
+            }
+    };
+
+    // a full stage, software-pipelined by one sub-tile: the S MFMAs of sub-tile
+    // rt+1 are independent of sub-tile rt's exp/split VALU work and overlap it
+    auto stage_full = [&](int64_t t0, const char* tl, const float* tls) {
+        s16x8 af[S16];
+        load_s(tl, 0, af);
+        f32x16 acc = mma_s(af);
+#pragma unroll
+        for (int rt = 0; rt < G::SUB; ++rt) {
+            const int64_t sub0 = t0 + rt * 32;
+            f32x16 acc_n = {};
+            if constexpr (PASS == LSE) {
+                if (rt + 1 < G::SUB) {
+                    load_s(tl, rt + 1, af);
+                    acc_n = mma_s(af);
+                }
+                lse_update(acc, sub0, 32);
+            } else {
+                s16x8 ga[G::DB][2];
+                load_g(tl, rt, ga);
+                if (rt + 1 < G::SUB) {
+                    load_s(tl, rt + 1, af);
+                    acc_n = mma_s(af);
+                }
+                s16x8 bh[2], bl[2];
+                make_ds(acc, tls, rt, sub0, 32, bh, bl);
+                mma_g(ga, bh, bl);
+            }
+            acc = acc_n;
+        }
+    };
+    // the split's last, partial stage: sub-tile by sub-tile with row masks
+    auto stage_tail = [&](int64_t t0, const char* tl, const float* tls) {
+#pragma unroll
+        for (int rt = 0; rt < G::SUB; ++rt) {
+            const int64_t sub0 = t0 + rt * 32;
+            if (sub0 >= i_end) break;  // block-uniform
+            const int left = static_cast<int>(i_end - sub0 < 32 ? i_end - sub0 : 32);
+            s16x8 af[S16];
+            load_s(tl, rt, af);
+            const f32x16 acc = mma_s(af);
+            if constexpr (PASS == LSE) {
+                lse_update(acc, sub0, left);
+            } else {
+                s16x8 ga[G::DB][2];
+                load_g(tl, rt, ga);
+                s16x8 bh[2], bl[2];
+                make_ds(acc, tls, rt, sub0, left, bh, bl);
+                mma_g(ga, bh, bl);
+            }
+        }
+    };
+
+    // full stages in the loop, the partial one after it: one path through the
+    // loop body keeps the accumulators in one register assignment
     if (i_begin < i_end) fetch(i_begin, 0);
     raw_barrier();
     int cur = 0;
-    for (int64_t t0 = i_begin; t0 < i_end; t0 += NT) {
-        const char* tl = tile[cur];
+    const int64_t t_full = i_begin + (i_end - i_begin) / NT * NT;  // end of the full stages
+    int64_t t0 = i_begin;
+    for (; t0 < t_full; t0 += NT) {
         if (t0 + NT < i_end) fetch(t0 + NT, cur ^ 1);
-#pragma unroll
-        for (int rt = 0; rt < NT / 32; ++rt) {
-            const int64_t sub0 = t0 + rt * 32;
-            if (sub0 >= i_end) break;  // block-uniform
-            // ---- S tile: acc[r] = <stream row sub0 + tile_row(r,h), fixed row f> ----
-            f32x16 acc = {};
-            {
-                const int row = rt * 32 + col;
-#pragma unroll
-                for (int s = 0; s < S16; ++s) {
-                    const int cg = 2 * s + h;
-                    const s16x8 af = __builtin_bit_cast(
-                        s16x8, *reinterpret_cast<const uint4*>(tl + img_off(cg >> 4, row, cg & 15)));
-                    acc = MM::run(af, qf[s], acc);
-                }
-            }
-            const int left = static_cast<int>(i_end - sub0 < 32 ? i_end - sub0 : 32);
-            if constexpr (PASS == LSE) {
-                float x[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) x[r] = acc[r] * a.c2;
-                if (left < 32) {  // partial last sub-tile (block-uniform)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (tile_row(r, h) >= left) x[r] = -INFINITY;
-                }
-                float mx = x[0];
-#pragma unroll
-                for (int r = 1; r < 16; ++r) mx = fmaxf(mx, x[r]);
-                const float mn = fmaxf(run_m, mx);
-                // raw v_exp_f32: arguments are <= 0, results below 2^-126 flush to 0
-                // (negligible next to the max term's 1)
-                float s = (mn == -INFINITY) ? 0.f : run_s * __builtin_amdgcn_exp2f(run_m - mn);
-#pragma unroll
-                for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(x[r] - mn);
-                run_m = mn;
-                run_s = s;
-                // label column: stream row f + off
-                const int64_t rr = f + a.off - sub0;
-                if (fok && rr >= 0 && rr < 32 && ((rr >> 2) & 1) == h) {
-                    const int rsel = static_cast<int>((rr & 3) + 4 * (rr >> 3));
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (r == rsel) dg = x[r];
-                }
-            } else {
-                // ---- dS = w·(2^(x − lse2_user) − [label]) in registers, as bf16 hi + lo ----
-                float lse_r[16];
-                if constexpr (PASS == COL) {  // users are the streamed rows: lse2 per row, from LDS
-                    const float* tls = tlse[cur] + rt * 32;
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        const float4 v = *reinterpret_cast<const float4*>(tls + 8 * g + 4 * h);
-                        lse_r[4 * g] = v.x; lse_r[4 * g + 1] = v.y; lse_r[4 * g + 2] = v.z; lse_r[4 * g + 3] = v.w;
-                    }
-                }
-                float ds[16];
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int tr = tile_row(r, h);
-                    const int64_t srow = sub0 + tr;
-                    const float l = (PASS == ROW) ? lse_f : lse_r[r];
-                    float e = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
-                    // label: ROW → stream item srow == user f + off; COL → item f == user srow + off
-                    const bool lab = (PASS == ROW) ? (srow == f + a.off) : (f == srow + a.off);
-                    if (lab) e -= 1.f;
-                    ds[r] = fok ? e * Split<T>::kScale : 0.f;
-                }
-                if (left < 32) {  // partial last sub-tile (block-uniform)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (tile_row(r, h) >= left) ds[r] = 0.f;
-                }
-                s16x8 bh[2], bl[2];
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    uint32_t hp[4], lp[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) Split<T>::run(ds[8 * s2 + 2 * j], ds[8 * s2 + 2 * j + 1], hp[j], lp[j]);
-                    bh[s2] = __builtin_bit_cast(s16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
-                    bl[s2] = __builtin_bit_cast(s16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
-                }
-                // ---- gradient: gaccᵀ[d][f] += Σ_rows X[row][d] · dS[row][f] ----
-                // A = Xᵀ fragment by transposed reads: element j of half h = row 16·s2 + 8(j>>2) + 4h + (j&3)
-                const int g16 = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
-#pragma unroll
-                for (int dbi = 0; dbi < G::DB; ++dbi) {
-                    const int db = db0 + dbi;
-                    const int half = db >> 2;
-                    const int c0 = ((db & 3) * 32 + 16 * (g16 & 1)) >> 3;  // chunk of the group's 16 columns
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        const int r0 = rt * 32 + 16 * s2 + 4 * h;
-                        const s16x4 lo4 = tr_read(tl, img_off(half, r0 + q, c0 + (p >> 1)) + 8 * (p & 1));
-                        const s16x4 hi4 = tr_read(tl, img_off(half, r0 + 8 + q, c0 + (p >> 1)) + 8 * (p & 1));
-                        const s16x8 af = s16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-                        gacc[dbi] = MM::run(af, bh[s2], gacc[dbi]);
-                        gacc[dbi] = MM::run(af, bl[s2], gacc[dbi]);
-                    }
-                }
-            }
-        }
+        stage_full(t0, tile[cur], tlse[cur]);
         raw_barrier();
         cur ^= 1;
     }
+    if (t0 < i_end) stage_tail(t0, tile[cur], tlse[cur]);
 
     if constexpr (PASS == LSE) {
         // merge the two lane halves (same fixed row), write the split's partial
@@ -336,17 +448,17 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             }
         }
     } else {
-        // gaccᵀ[db][r] = grad[d = 32db + tile_row(r,h)][fixed row f] → partial [split][f][DP]
+        // gaccᵀ[db][r] = grad[d = 32db + krow(r) + 4h][fixed row f] → partial [split][f][DP]
         if (fok) {
             const float gs = a.inv_tau * a.w / Split<T>::kScale;
             float* gp = a.gpart + (static_cast<int64_t>(split) * a.n_fixed + f) * DP;
 #pragma unroll
-            for (int dbi = 0; dbi < G::DB; ++dbi)
+            for (int db = 0; db < G::DB; ++db)
 #pragma unroll
                 for (int g = 0; g < 4; ++g)
-                    *reinterpret_cast<float4*>(gp + 32 * (db0 + dbi) + 8 * g + 4 * h) =
-                        make_float4(gacc[dbi][4 * g] * gs, gacc[dbi][4 * g + 1] * gs, gacc[dbi][4 * g + 2] * gs,
-                                    gacc[dbi][4 * g + 3] * gs);
+                    *reinterpret_cast<float4*>(gp + 32 * db + 8 * g + 4 * h) =
+                        make_float4(gacc[db][4 * g] * gs, gacc[db][4 * g + 1] * gs, gacc[db][4 * g + 2] * gs,
+                                    gacc[db][4 * g + 3] * gs);
         }
     }
 }
@@ -380,9 +492,12 @@ __global__ __launch_bounds__(256) void ib16_finalize_kernel(const float2* __rest
     }
 }
 
-// out[r][c] = Σ_s part[s][r][c] (fixed order), for c < d (part rows are DP wide)
+// out[r][c] = Σ_s part[s][r][c] (fixed order) − coef·lab[r + lab_off][c] (the
+// label term of dS = softmax − I, when row r + lab_off of lab exists), c < d
+template <typename T>
 __global__ __launch_bounds__(256) void ib16_reduce_kernel(const float* __restrict__ part, int splits, int64_t rows,
-                                                          int dp, int d, float* __restrict__ out) {
+                                                          int dp, int d, const T* __restrict__ lab, int64_t lab_off,
+                                                          int64_t lab_rows, float coef, float* __restrict__ out) {
     const int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
     const int64_t total = rows * d;
     if (e >= total) return;
@@ -393,12 +508,20 @@ __global__ __launch_bounds__(256) void ib16_reduce_kernel(const float* __restric
         const float4 v = *reinterpret_cast<const float4*>(part + (static_cast<int64_t>(s) * rows + r) * dp + c);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
+    const int64_t lr = r + lab_off;
+    if (lr >= 0 && lr < lab_rows) {
+        const T* l = lab + lr * d + c;
+        acc.x -= coef * static_cast<float>(l[0]);
+        acc.y -= coef * static_cast<float>(l[1]);
+        acc.z -= coef * static_cast<float>(l[2]);
+        acc.w -= coef * static_cast<float>(l[3]);
+    }
     *reinterpret_cast<float4*>(out + e) = acc;
 }
 
-inline int splits_for(int64_t fixed_blocks, int64_t n_stream) {
-    int64_t s = (256 + fixed_blocks - 1) / fixed_blocks;  // ~1 block (8 waves) per CU
-    const int64_t mx = (n_stream + 4 * NT - 1) / (4 * NT);  // >= 4 stages per split
+inline int splits_for(int64_t fixed_blocks, int64_t n_stream, int nt) {
+    int64_t s = (256 + fixed_blocks - 1) / fixed_blocks;  // ~1 block per CU
+    const int64_t mx = (n_stream + 4 * nt - 1) / (4 * nt);  // >= 4 stages per split
     if (s > mx) s = mx;
     if (s > 64) s = 64;
     return static_cast<int>(s < 1 ? 1 : s);
@@ -410,11 +533,11 @@ struct PassPlan {
     int64_t per;  // streamed rows per split (multiple of NT)
 };
 
-inline PassPlan pass_plan(int64_t n_fixed, int64_t n_stream, int ft) {
+inline PassPlan pass_plan(int64_t n_fixed, int64_t n_stream, int ft, int nt) {
     PassPlan q{};
     q.fixed_blocks = (n_fixed + ft - 1) / ft;
-    q.splits = splits_for(q.fixed_blocks, n_stream);
-    q.per = ((n_stream + q.splits - 1) / q.splits + NT - 1) / NT * NT;
+    q.splits = splits_for(q.fixed_blocks, n_stream, nt);
+    q.per = ((n_stream + q.splits - 1) / q.splits + nt - 1) / nt * nt;
     q.splits = static_cast<int>((n_stream + q.per - 1) / q.per);
     return q;
 }
@@ -425,24 +548,29 @@ struct Plan {
     size_t part_off, diag_off, lse_off, gp_off, bytes;
 };
 
-inline Plan make_plan(int64_t b, int64_t nx, int d) {
+template <int DP>
+inline Plan make_plan_t(int64_t b, int64_t nx) {
     Plan p{};
-    p.dp = d <= 128 ? 128 : 256;
-    const int ft_l = 256, ft_g = p.dp <= 128 ? 256 : 128;  // Geo<DP, PASS>::FT
-    p.lse = pass_plan(b, nx, ft_l);
-    p.row = pass_plan(b, nx, ft_g);
-    p.col = pass_plan(nx, b, ft_g);
+    p.dp = DP;
+    p.lse = pass_plan(b, nx, Geo<DP, LSE>::FT, Geo<DP, LSE>::NT);
+    p.row = pass_plan(b, nx, Geo<DP, ROW>::FT, Geo<DP, ROW>::NT);
+    p.col = pass_plan(nx, b, Geo<DP, COL>::FT, Geo<DP, COL>::NT);
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     size_t o = 0;
     p.part_off = o; o += al(static_cast<size_t>(p.lse.splits) * b * sizeof(float2));
     p.diag_off = o; o += al(static_cast<size_t>(b) * sizeof(float));
-    p.lse_off = o; o += al(static_cast<size_t>((b + 63) / 64 * 64 + 64) * sizeof(float));  // DMA-padded
+    // the COL pass DMAs NT lse2 values per stage: padded past b by a whole stage
+    p.lse_off = o; o += al(static_cast<size_t>((b + 255) / 256 * 256 + 256) * sizeof(float));
     p.gp_off = o;
-    const size_t g_row = static_cast<size_t>(p.row.splits) * b * p.dp * sizeof(float);
-    const size_t g_col = static_cast<size_t>(p.col.splits) * nx * p.dp * sizeof(float);
+    const size_t g_row = static_cast<size_t>(p.row.splits) * b * DP * sizeof(float);
+    const size_t g_col = static_cast<size_t>(p.col.splits) * nx * DP * sizeof(float);
     o += al(g_row > g_col ? g_row : g_col);
     p.bytes = o;
     return p;
+}
+
+inline Plan make_plan(int64_t b, int64_t nx, int d) {
+    return d <= 128 ? make_plan_t<128>(b, nx) : make_plan_t<256>(b, nx);
 }
 
 }  // namespace ib16
@@ -481,16 +609,17 @@ static int ib16_run_t(const void* u, const void* p, int64_t b, int64_t nx, int d
     a.splits = pl.row.splits; a.per_split = pl.row.per;
     hipLaunchKernelGGL((ib16_kernel<T, DP, ROW>), grid(pl.row), blk_r, 0, st, a);
     if ((rc = check_launch("ib16_kernel<row>"))) return rc;
-    hipLaunchKernelGGL(ib16_reduce_kernel, dim3(static_cast<unsigned>((b * d / 4 + 255) / 256)), dim3(256), 0, st,
-                       a.gpart, pl.row.splits, b, DP, d, du);
+    const float coef = inv_tau * a.w;  // d L/d S_label = −w, times 1/τ
+    hipLaunchKernelGGL(ib16_reduce_kernel<T>, dim3(static_cast<unsigned>((b * d / 4 + 255) / 256)), dim3(256), 0, st,
+                       a.gpart, pl.row.splits, b, DP, d, reinterpret_cast<const T*>(p), off, nx, coef, du);
     if ((rc = check_launch("ib16_reduce_kernel(du)"))) return rc;
     // column pass: dP (items fixed, users streamed)
     a.fixed = p; a.stream = u; a.n_fixed = nx; a.n_stream = b;
     a.splits = pl.col.splits; a.per_split = pl.col.per;
     hipLaunchKernelGGL((ib16_kernel<T, DP, COL>), grid(pl.col), blk_c, 0, st, a);
     if ((rc = check_launch("ib16_kernel<col>"))) return rc;
-    hipLaunchKernelGGL(ib16_reduce_kernel, dim3(static_cast<unsigned>((nx * d / 4 + 255) / 256)), dim3(256), 0, st,
-                       a.gpart, pl.col.splits, nx, DP, d, dp);
+    hipLaunchKernelGGL(ib16_reduce_kernel<T>, dim3(static_cast<unsigned>((nx * d / 4 + 255) / 256)), dim3(256), 0, st,
+                       a.gpart, pl.col.splits, nx, DP, d, reinterpret_cast<const T*>(u), -off, b, coef, dp);
     return check_launch("ib16_reduce_kernel(dp)");
 }
 
