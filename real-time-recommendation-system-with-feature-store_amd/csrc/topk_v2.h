@@ -409,6 +409,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
                 typename M::frag af[S];
 #pragma unroll
                 for (int s = 0; s < S; ++s) af[s] = frag_from<T>(arow + ((2 * s + half) ^ C::swz(row)) * VEC);
+                __builtin_amdgcn_sched_barrier(0);  // every read in flight before the first MFMA waits
 #pragma unroll
                 for (int s = 0; s < S; ++s) acc = M::run(af[s], qf[s], acc);
             }
