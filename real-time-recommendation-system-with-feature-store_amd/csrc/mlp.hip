@@ -548,19 +548,20 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
 // backward 2: dW[n][k] += Σ_r dz[r][n] · A[r][k] (+ dbias[n] += Σ_r dz[r][n]),
 // M split over blockIdx.z
 // ---------------------------------------------------------------------------
-// Every wave owns a 64(n) x 32·KT(k) tile (2·KT independent 32x32 accumulators)
-// over its own contiguous slice of the block's rows, so the main loop has no
-// barrier: each k-step (2 rows) a lane loads dz[r][n0+c32], dz[r][n0+32+c32]
-// and A[r][k0+32j+c32] straight from L2/HBM (128 B per half-wave), groups of
-// U k-steps are double-buffered in registers (the next group's loads fly
-// during the current group's MFMAs), and the A prologue (act → BN affine →
-// dropout) runs on registers with per-lane column constants. The 4 waves'
-// tiles are summed through LDS and added to dW with one fp32 atomic per
-// element per block (<= 32 splits, see the host).
+// Block = one 64(n) x 64(k) tile of dW over a contiguous row range, 4 waves
+// each owning a 32 x 32 quarter. Rows stream in chunks of 64: every thread
+// loads a float4 of dz and of A for 4 rows (global loads of chunk c+1 are in
+// flight while chunk c is multiplied), applies the A prologue (act → BN
+// affine → dropout, the forward's own transform) on registers and writes both
+// tiles TRANSPOSED into LDS ([col][row], 16-B aligned rows), so each lane's
+// MFMA operands are contiguous: lane half h reduces rows h·32 + s, and one
+// ds_read_b128 feeds 4 v_mfma_f32_32x32x2_f32 k-steps. The tile is added to
+// dW with one fp32 atomic per element per block (<= 32 splits, see the host).
 //   PRO: 0 raw A, 1 piecewise-linear act, 2 same + dropout, 3 generic act.
-constexpr int DW_N = 64;      // n per block/wave
-constexpr int DW_SEG = 2048;  // rows whose gather ids are staged in LDS at a time
-constexpr int DW_U = 4;       // k-steps (2 rows each) per register group
+constexpr int DW_T = 64;          // n and k per block
+constexpr int DW_R = 64;          // rows per chunk
+constexpr int DW_LD = DW_R + 4;   // LDS row stride (floats) of the transposed tiles
+constexpr int DW_MAXR = 4096;     // rows per split whose gather ids are staged in LDS
 
 template <int PRO>
 __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, int c, float sc, float sh, float v) {
@@ -578,140 +579,137 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
     }
 }
 
-template <int KT, int PRO>
+template <int PRO, bool VEC>  // VEC: n, k, ld_src multiples of 4 and 16-B aligned rows
 __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a, int64_t rows_per_split) {
-    constexpr int NT = 2, U = DW_U;
-    constexpr int NV = NT * KT * 16;  // accumulator registers per lane
-    __shared__ int srow[DW_SEG];
-    __shared__ float red[4][NV][64];
-    __shared__ float bred[4][DW_N];
+    __shared__ __attribute__((aligned(16))) float dzT[DW_T][DW_LD];
+    __shared__ __attribute__((aligned(16))) float aT[DW_T][DW_LD];
+    __shared__ int srow[DW_MAXR];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int n0 = blockIdx.x * DW_N, k0 = blockIdx.y * (32 * KT);
+    const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
     const int64_t r_begin = static_cast<int64_t>(blockIdx.z) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
-
-    int gn[NT], gk[KT];
-    bool n_ok[NT], k_ok[KT];
-    // BN affine of the previous block per column, per row segment (two BN batches)
-    float sc[2][KT], sh[2][KT];
+    const bool gather = a.ids != nullptr;
     const bool two = a.seg_split > 0;
+
+    // staging role: 4 consecutive columns (c4) of rows rr + 16p, p = 0..3
+    const int c4 = tid >> 4, rr = tid & 15;
+    const int gn = n0 + 4 * c4, gk = k0 + 4 * c4;
+    // BN affine of the previous block for this thread's 4 A columns, per row segment
+    float sc[2][4], sh[2][4];
 #pragma unroll
-    for (int i = 0; i < NT; ++i) { gn[i] = n0 + 32 * i + c32; n_ok[i] = gn[i] < n; }
+    for (int sg = 0; sg < 2; ++sg)
 #pragma unroll
-    for (int j = 0; j < KT; ++j) {
-        gk[j] = k0 + 32 * j + c32;
-        k_ok[j] = gk[j] < k;
-#pragma unroll
-        for (int sg = 0; sg < 2; ++sg) {
-            sc[sg][j] = 1.f; sh[sg][j] = 0.f;
+        for (int i = 0; i < 4; ++i) {
+            sc[sg][i] = 1.f;
+            sh[sg][i] = 0.f;
+            const int c = gk + i;
             const int so = two ? sg * k : 0;
-            if ((a.prev_mode == 1 || a.prev_mode == 2) && k_ok[j])
-                bn_affine(a.prev_gamma[gk[j]], a.prev_beta[gk[j]], a.prev_mean[so + gk[j]], a.prev_invstd[so + gk[j]],
-                          sc[sg][j], sh[sg][j]);
+            if ((a.prev_mode == 1 || a.prev_mode == 2) && c < k)
+                bn_affine(a.prev_gamma[c], a.prev_beta[c], a.prev_mean[so + c], a.prev_invstd[so + c], sc[sg][i],
+                          sh[sg][i]);
         }
-    }
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
                   pseed, nullptr, nullptr};
     const float slope = act_slope(a.prev_act);
     const bool do_bias = a.dbias != nullptr && blockIdx.y == 0;
-    const bool gather = a.ids != nullptr;
 
-    f32x16 acc[NT][KT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int j = 0; j < KT; ++j) acc[i][j] = f32x16{};
-    float bsum[NT] = {};
+    if (gather) {
+        for (int64_t t = tid; t < r_end - r_begin; t += 256) {
+            const int64_t id = a.ids[r_begin + t];
+            srow[t] = (id < 0 || id >= a.src_rows) ? -1 : static_cast<int>(id);
+        }
+        __syncthreads();
+    }
 
-    float dA[U][NT], xA[U][KT], dB[U][NT], xB[U][KT];
-    int64_t seg0 = 0;
-    auto load = [&](float (&d)[U][NT], float (&x)[U][KT], int64_t g, int64_t we) {
+    float4 dv[4], av[4];  // one chunk's staged values (prefetch registers)
+    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x16 acc = f32x16{};
+    const float* ar = &dzT[(w & 1) * 32 + c32][h * 32];
+    const float* br = &aT[(w >> 1) * 32 + c32][h * 32];
+    auto load = [&](int64_t nx) {  // one chunk's dz / A float4s into registers
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t r = g + 2 * u + h;
-            const bool rv = r < we;
-            int64_t sr = r;
-            if (gather) sr = rv ? srow[r - seg0] : -1;
-#pragma unroll
-            for (int i = 0; i < NT; ++i) d[u][i] = (rv && n_ok[i]) ? a.dz_ws[r * n + gn[i]] : 0.f;
-#pragma unroll
-            for (int j = 0; j < KT; ++j) x[u][j] = (rv && sr >= 0 && k_ok[j]) ? a.src[sr * a.ld_src + gk[j]] : 0.f;
+        for (int p = 0; p < 4; ++p) {
+            const int64_t r = nx + rr + 16 * p;
+            dv[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            av[p] = dv[p];
+            if (r >= r_end) continue;
+            const float* dz = a.dz_ws + r * n + gn;
+            const int64_t sr = gather ? srow[r - r_begin] : r;
+            const float* ap = a.src + sr * a.ld_src + gk;
+            if constexpr (VEC) {
+                if (gn < n) dv[p] = *reinterpret_cast<const float4*>(dz);
+                if (gk < k && sr >= 0) av[p] = *reinterpret_cast<const float4*>(ap);
+            } else {
+                if (gn < n) dv[p].x = dz[0];
+                if (gn + 1 < n) dv[p].y = dz[1];
+                if (gn + 2 < n) dv[p].z = dz[2];
+                if (gn + 3 < n) dv[p].w = dz[3];
+                if (sr >= 0) {
+                    if (gk < k) av[p].x = ap[0];
+                    if (gk + 1 < k) av[p].y = ap[1];
+                    if (gk + 2 < k) av[p].z = ap[2];
+                    if (gk + 3 < k) av[p].w = ap[3];
+                }
+            }
         }
     };
-    auto compute = [&](float (&d)[U][NT], float (&x)[U][KT], int64_t g) {
+    if (r_begin < r_end) load(r_begin);
+    for (int64_t c0 = r_begin; c0 < r_end; c0 += DW_R) {
+        __syncthreads();  // the previous chunk's MFMA reads are done
+        // stage: dz as is, A through the prologue, both transposed into LDS
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t r = g + 2 * u + h;
+        for (int p = 0; p < 4; ++p) {
+            const int row = rr + 16 * p;
+            const int64_t r = c0 + row;
+            const bool hi_seg = two && r >= a.seg_split;
+            const bool ok = r < r_end && (!gather || srow[r - r_begin] >= 0);
+            const float d4[4] = {dv[p].x, dv[p].y, dv[p].z, dv[p].w};
+            const float a4[4] = {av[p].x, av[p].y, av[p].z, av[p].w};
 #pragma unroll
-            for (int j = 0; j < KT; ++j) {
-                const int sg = (two && r >= a.seg_split) ? 1 : 0;
-                const float xa = pro_col<PRO>(pro, slope, r, gk[j], sg ? sc[1][j] : sc[0][j], sg ? sh[1][j] : sh[0][j],
-                                              x[u][j]);
-#pragma unroll
-                for (int i = 0; i < NT; ++i) acc[i][j] = mfma(d[u][i], xa, acc[i][j]);
-            }
-            if (do_bias) {
-#pragma unroll
-                for (int i = 0; i < NT; ++i) bsum[i] += d[u][i];
+            for (int i = 0; i < 4; ++i) {
+                dzT[4 * c4 + i][row] = d4[i];
+                bsum[i] += d4[i];
+                const float scv = hi_seg ? sc[1][i] : sc[0][i], shv = hi_seg ? sh[1][i] : sh[0][i];
+                aT[4 * c4 + i][row] = (ok && gk + i < k) ? pro_col<PRO>(pro, slope, r, gk + i, scv, shv, a4[i]) : 0.f;
             }
         }
-    };
-
-    for (seg0 = r_begin; seg0 < r_end; seg0 += DW_SEG) {
-        const int64_t seg1 = (seg0 + DW_SEG) < r_end ? (seg0 + DW_SEG) : r_end;
-        if (gather) {
-            __syncthreads();
-            for (int t = tid; t < seg1 - seg0; t += 256) {
-                const int64_t id = a.ids[seg0 + t];
-                srow[t] = (id < 0 || id >= a.src_rows) ? -1 : static_cast<int>(id);
-            }
-            __syncthreads();
-        }
-        // this wave's contiguous slice of the segment (multiple of 2U rows)
-        const int64_t len = seg1 - seg0;
-        const int64_t per = ((len + 3) / 4 + 2 * U - 1) / (2 * U) * (2 * U);
-        const int64_t wb = seg0 + w * per;
-        const int64_t we = (wb + per) < seg1 ? (wb + per) : seg1;
-        if (wb >= we) continue;
-        load(dA, xA, wb, we);
-        for (int64_t g = wb; g < we; g += 4 * U) {
-            if (g + 2 * U < we) load(dB, xB, g + 2 * U, we);
-            compute(dA, xA, g);
-            if (g + 2 * U >= we) break;
-            if (g + 4 * U < we) load(dA, xA, g + 4 * U, we);
-            compute(dB, xB, g + 2 * U);
+        __syncthreads();
+        // next chunk's loads fly during this chunk's MFMAs
+        if (c0 + DW_R < r_end) load(c0 + DW_R);
+#pragma unroll
+        for (int s = 0; s < 32; s += 4) {
+            const float4 x = *reinterpret_cast<const float4*>(ar + s);
+            const float4 y = *reinterpret_cast<const float4*>(br + s);
+            acc = mfma(x.x, y.x, acc);
+            acc = mfma(x.y, y.y, acc);
+            acc = mfma(x.z, y.z, acc);
+            acc = mfma(x.w, y.w, acc);
         }
     }
 
-    // ---- sum the 4 waves' tiles through LDS, one atomic per element ----
+    // acc[r] = dW[n0 + 32(w&1) + (r&3) + 8(r>>2) + 4h][k0 + 32(w>>1) + c32]
+    const int ok_k = k0 + (w >> 1) * 32 + c32;
+    if (ok_k < k) {
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int j = 0; j < KT; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) red[w][(i * KT + j) * 16 + r][lane] = acc[i][j][r];
-    if (do_bias) {
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            const float t = bsum[i] + __shfl_xor(bsum[i], 32, 64);
-            if (h == 0) bred[w][32 * i + c32] = t;
+        for (int r = 0; r < 16; ++r) {
+            const int on = n0 + (w & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (on < n) atomicAdd(&a.dw[static_cast<int64_t>(on) * k + ok_k], acc[r]);
         }
     }
-    __syncthreads();
-    for (int p = tid; p < NV * 64; p += 256) {
-        const int v = p >> 6, l = p & 63;
-        const float t = red[0][v][l] + red[1][v][l] + red[2][v][l] + red[3][v][l];
-        const int i = v / (KT * 16), j = (v / 16) % KT, rr = v & 15;
-        const int on = n0 + 32 * i + (rr & 3) + 8 * (rr >> 2) + 4 * (l >> 5);
-        const int ok = k0 + 32 * j + (l & 31);
-        if (on < n && ok < k) atomicAdd(&a.dw[static_cast<int64_t>(on) * k + ok], t);
-    }
-    if (do_bias && tid < DW_N) {
-        const int col = n0 + tid;
-        if (col < n) atomicAdd(&a.dbias[col], bred[0][tid] + bred[1][tid] + bred[2][tid] + bred[3][tid]);
+    if (do_bias) {  // the 16 threads of a column group are 16 consecutive lanes
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int o = 1; o < 16; o <<= 1) bsum[i] += __shfl_xor(bsum[i], o, 64);
+        }
+        if (rr == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (gn + i < n) atomicAdd(&a.dbias[gn + i], bsum[i]);
+        }
     }
 }
 
@@ -809,27 +807,31 @@ extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream
     const rt_linear_bwd_args& a = *args;
     if (a.m == 0) return RT_OK;
     hipStream_t st = as_stream(stream);
-    const int kt = a.k <= 32 ? 1 : 2;
-    const int tn = (a.n + mlp::DW_N - 1) / mlp::DW_N;
-    const int tk = (a.k + 32 * kt - 1) / (32 * kt);
-    // ~512 blocks (2 per CU), >= 64 rows per block, <= 32 splits per tile
+    const int tn = (a.n + mlp::DW_T - 1) / mlp::DW_T;
+    const int tk = (a.k + mlp::DW_T - 1) / mlp::DW_T;
+    // ~512 blocks (2 per CU), whole 64-row chunks, <= 32 splits per tile (atomics
+    // per dW element), <= DW_MAXR rows per split (gather ids staged in LDS)
     int64_t splits = (512 + tn * tk - 1) / (tn * tk);
-    const int64_t max_splits = (a.m + 63) / 64;
+    const int64_t max_splits = (a.m + mlp::DW_R - 1) / mlp::DW_R;
     if (splits > max_splits) splits = max_splits;
     if (splits > 32) splits = 32;
     if (splits < 1) splits = 1;
     int64_t rps = (a.m + splits - 1) / splits;
-    rps = (rps + 63) / 64 * 64;
+    rps = (rps + mlp::DW_R - 1) / mlp::DW_R * mlp::DW_R;
+    if (a.ids && rps > mlp::DW_MAXR) rps = mlp::DW_MAXR;
     splits = (a.m + rps - 1) / rps;
+    if (splits > 65535) return RT_ERR_UNSUPPORTED;
     const dim3 grid(static_cast<unsigned>(tn), static_cast<unsigned>(tk), static_cast<unsigned>(splits));
     int pro = 0;
     if (a.prev_mode != 0)
         pro = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
-#define RT_DW(KT, P) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<KT, P>), grid, dim3(256), 0, st, a, rps)
-    if (kt == 1) {
-        switch (pro) { case 0: RT_DW(1, 0); break; case 1: RT_DW(1, 1); break; case 2: RT_DW(1, 2); break; default: RT_DW(1, 3); }
+    const bool vec = (a.n % 4) == 0 && (a.k % 4) == 0 && (a.ld_src % 4) == 0 &&
+                     (reinterpret_cast<uintptr_t>(a.src) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dz_ws) & 15) == 0;
+#define RT_DW(P, V) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<P, V>), grid, dim3(256), 0, st, a, rps)
+    if (vec) {
+        switch (pro) { case 0: RT_DW(0, true); break; case 1: RT_DW(1, true); break; case 2: RT_DW(2, true); break; default: RT_DW(3, true); }
     } else {
-        switch (pro) { case 0: RT_DW(2, 0); break; case 1: RT_DW(2, 1); break; case 2: RT_DW(2, 2); break; default: RT_DW(2, 3); }
+        switch (pro) { case 0: RT_DW(0, false); break; case 1: RT_DW(1, false); break; case 2: RT_DW(2, false); break; default: RT_DW(3, false); }
     }
 #undef RT_DW
     return check_launch("linear_bwd_dw_kernel");

@@ -11,6 +11,7 @@ accumulated straight into one flat fp32 grad slab (views are the params'
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import itertools
 from dataclasses import dataclass, field
@@ -314,9 +315,15 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
 
 def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab: ParamSlab,
                    want_dsrc: bool = False, seed_offset: Optional[torch.Tensor] = None,
-                   stats_arena: Optional[torch.Tensor] = None, attach: bool = True) -> Optional[torch.Tensor]:
+                   stats_arena: Optional[torch.Tensor] = None, attach: bool = True,
+                   dw_stream: Optional[torch.cuda.Stream] = None) -> Optional[torch.Tensor]:
     """Backward through the chain; parameter grads are atomically accumulated
-    into the slab. Returns d src (dense input) when ``want_dsrc``."""
+    into the slab. Returns d src (dense input) when ``want_dsrc``.
+
+    With ``dw_stream`` every layer's dW launch runs on that stream after its dz
+    launch (one event each), overlapping the dz launch of the layer below on
+    the current stream (each layer then keeps its own dz buffer); the current
+    stream joins ``dw_stream`` before returning."""
     dev = dout.device
     dout = dout.contiguous()
     m = ctx.m
@@ -325,7 +332,8 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
     if attach:
         slab.attach_grads()
     max_w = max(b.linear.out_features for b in blocks)
-    dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev)
+    dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev) if dw_stream is None else None
+    keep = []  # per-layer dz buffers read by the dW launches on dw_stream
     widths = [b.linear.out_features for b in blocks[:-1]]
     n_seg = 2 if ctx.seg_split else 1
     gst_arena = stats_arena if stats_arena is not None else \
@@ -344,7 +352,11 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         a.w = lin.weight.data_ptr()
         a.dw = slab.grad_of(lin.weight).data_ptr()
         a.dbias = slab.grad_of(lin.bias).data_ptr() if lin.bias is not None else None
-        a.dz_ws = dz_ws.data_ptr()
+        if dw_stream is None:
+            a.dz_ws = dz_ws.data_ptr()
+        else:
+            keep.append(torch.empty((m, lin.out_features), dtype=torch.float32, device=dev))
+            a.dz_ws = keep[-1].data_ptr()
         a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
         a.seg_split = ctx.seg_split
         if li == L:
@@ -404,7 +416,14 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         with TIMER.region("linear_bwd_dz", flops=(2.0 if da else 0.0) * m * a.k * a.n,
                           bytes_=4.0 * (3 * m * a.n + (2 * m * a.k if da else 0) + a.n * a.k)):
             call("rt_linear_bwd_dz_f32", ctypes.byref(a), st)
-        with TIMER.region("linear_bwd_dw", flops=2.0 * m * a.k * a.n,
-                          bytes_=4.0 * (m * a.n + m * a.k + a.n * a.k)):
-            call("rt_linear_bwd_dw_f32", ctypes.byref(a), st)
+        if dw_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            dw_stream.wait_event(ev)
+        with torch.cuda.stream(dw_stream) if dw_stream is not None else contextlib.nullcontext():
+            with TIMER.region("linear_bwd_dw", flops=2.0 * m * a.k * a.n,
+                              bytes_=4.0 * (m * a.n + m * a.k + a.n * a.k)):
+                call("rt_linear_bwd_dw_f32", ctypes.byref(a), _stream(dout))
+    if dw_stream is not None:
+        torch.cuda.current_stream(dev).wait_stream(dw_stream)
     return dsrc
