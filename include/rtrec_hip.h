@@ -231,6 +231,16 @@ int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);
  * order on one stream): dz/dgamma/dbeta/dA, then dW/dbias from dz_ws. */
 int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream);
 int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream);
+/* Up to two independent Linears in ONE launch (n_args = 1 or 2; e.g. layer l
+ * of the user and of the item tower): the same arguments and results as n_args
+ * separate calls, with both layers' work sharing the GPU at once (a replayed
+ * hipGraph runs parallel stream branches one after the other, so the two
+ * towers' chains only overlap when their launches are merged).
+ * Replaces the concurrent UserTower/ItemTower calls of the trainer step
+ * (src/training/trainers/two_tower.py:104-137). */
+int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_args, void* stream);
+int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream);
+int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream);
 
 /* ------------------------------------------------------------------------
  * Losses (fp32 scores, fp32 accumulation; bf16/f16 inputs widened on load).

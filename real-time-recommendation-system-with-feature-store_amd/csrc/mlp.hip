@@ -25,6 +25,21 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr float kNormEps = 1e-12f;
 
+// Up to two independent Linears (the user and the item tower's layer l) in ONE
+// launch: blocks [0, split) run a0, the rest a1 — the two chains overlap
+// without relying on concurrent streams (a replayed hipGraph runs its parallel
+// branches one after the other).
+struct FwdLaunch {
+    rt_linear_fwd_args a0, a1;
+    unsigned split;
+};
+struct BwdLaunch {
+    rt_linear_bwd_args a0, a1;
+    unsigned split;
+    int64_t rps0, rps1;     // dW: rows per split
+    unsigned tn0, tk0, tn1, tk1;  // dW: tile grid of each group
+};
+
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -87,7 +102,10 @@ constexpr int FM = 32;  // rows per block
 __host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // kh % 16 == 0
 
 template <int TPW, bool KVEC>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
-__global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
+__global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
+    const bool g1 = blockIdx.x >= L.split;
+    const rt_linear_fwd_args& a = g1 ? L.a1 : L.a0;
+    const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
     constexpr int NT = 4 * TPW;  // column tiles in the block
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int k = a.k, n = a.n;
@@ -99,7 +117,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
     int64_t* srow = reinterpret_cast<int64_t*>(rowpart + NT * FM);  // [FM]
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * FM;
+    const int64_t row0 = static_cast<int64_t>(bid) * FM;
     const int64_t m = a.m;
 
     // BatchNorm of the previous block: this block's batch is its row segment;
@@ -111,7 +129,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
         const int nseg = two ? 2 : 1;
         for (int c = tid; c < k; c += 256) {
             for (int sg = 0; sg < nseg; ++sg) {
-                if (blockIdx.x != 0 && sg != my_seg) continue;
+                if (bid != 0 && sg != my_seg) continue;
                 const int64_t ms = two ? (sg == 0 ? a.seg_split : m - a.seg_split) : m;
                 float mean, invstd, var_f = 0.f;
                 if (a.prev_mode == 1) {
@@ -129,7 +147,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
                     invstd = static_cast<float>(1.0 / sqrt(static_cast<double>(a.running_var[c]) + a.bn_eps));
                 }
                 if (sg == my_seg) bn_affine(a.bn_gamma[c], a.bn_beta[c], mean, invstd, scale[c], shift[c]);
-                if (blockIdx.x == 0) {
+                if (bid == 0) {
                     if (c == 0 && a.prev_mode == 1 && a.num_batches_tracked) *a.num_batches_tracked += 1;
                     if (a.save_mean) a.save_mean[sg * k + c] = mean;
                     if (a.save_invstd) a.save_invstd[sg * k + c] = invstd;
@@ -262,7 +280,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
     // ---- epilogue ----
     const bool l2 = a.l2_out != nullptr;
     double* const stats = a.stats_out ? a.stats_out + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
-                                                       blockIdx.x % RT_STAT_SLOTS) * 2 * n : nullptr;
+                                                       bid % RT_STAT_SLOTS) * 2 * n : nullptr;
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
         const int ct = w + 4 * i;
@@ -327,14 +345,17 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(rt_linear_fwd_args a) {
 // Block = 32 rows. dz (32 x n) lives in LDS; dA = dz·W reads W[n][k] rows
 // coalesced along k straight from L2 (the reduction runs over n).
 template <int TPWK>  // 32-col dA tiles per wave (k <= 128*TPWK)
-__global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a) {
+__global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
+    const bool g1 = blockIdx.x >= L.split;
+    const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
+    const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
     const int np = pad8(n), nh = np / 2, ldz = np + 4;
     float* Dz = sm;  // [FM][ldz]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int64_t row0 = static_cast<int64_t>(blockIdx.x) * FM;
+    const int64_t row0 = static_cast<int64_t>(bid) * FM;
     const bool two = a.seg_split > 0;
     const int my_seg = (two && row0 >= a.seg_split) ? 1 : 0;
     const int64_t seg_m = two ? (my_seg == 0 ? a.seg_split : m - a.seg_split) : m;
@@ -445,7 +466,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
             }
         }
     }
-    if (blockIdx.x == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
+    if (bid == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
         // dgamma/dbeta of each BN batch (segment), summed like two tower calls' grads
         for (int c = tid; c < n; c += 256) {
             for (int sg = 0; sg < (two ? 2 : 1); ++sg) {
@@ -506,7 +527,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
     double* const gps = want_stats ? a.g_prev_stats + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
-                                                        blockIdx.x % RT_STAT_SLOTS) * 2 * k : nullptr;
+                                                        bid % RT_STAT_SLOTS) * 2 * k : nullptr;
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
         const int kk = (w + 4 * i) * 32 + c32;
@@ -546,7 +567,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(rt_linear_bwd_args a
 
 // ---------------------------------------------------------------------------
 // backward 2: dW[n][k] += Σ_r dz[r][n] · A[r][k] (+ dbias[n] += Σ_r dz[r][n]),
-// M split over blockIdx.z
+// M split over the blocks of a group
 // ---------------------------------------------------------------------------
 // Block = one 64(n) x 64(k) tile of dW over a contiguous row range, 4 waves
 // each owning a 32 x 32 quarter. Rows stream in chunks of 64: every thread
@@ -580,15 +601,22 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
 }
 
 template <int PRO, bool VEC>  // VEC: n, k, ld_src multiples of 4 and 16-B aligned rows
-__global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a, int64_t rows_per_split) {
+__global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
+    const bool g1 = blockIdx.x >= L.split;
+    const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
+    const int64_t rows_per_split = g1 ? L.rps1 : L.rps0;
+    // flattened (n tile, k tile, split) of this block within its group
+    const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
+    const unsigned tn = g1 ? L.tn1 : L.tn0, tk = g1 ? L.tk1 : L.tk0;
+    const unsigned bx = bid % tn, by = (bid / tn) % tk, bz = bid / (tn * tk);
     __shared__ __attribute__((aligned(16))) float dzT[DW_T][DW_LD];
     __shared__ __attribute__((aligned(16))) float aT[DW_T][DW_LD];
     __shared__ int srow[DW_MAXR];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int n0 = blockIdx.x * DW_T, k0 = blockIdx.y * DW_T;
-    const int64_t r_begin = static_cast<int64_t>(blockIdx.z) * rows_per_split;
+    const int n0 = static_cast<int>(bx) * DW_T, k0 = static_cast<int>(by) * DW_T;
+    const int64_t r_begin = static_cast<int64_t>(bz) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
     const bool gather = a.ids != nullptr;
     const bool two = a.seg_split > 0;
@@ -597,24 +625,23 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a
     const int c4 = tid >> 4, rr = tid & 15;
     const int gn = n0 + 4 * c4, gk = k0 + 4 * c4;
     // BN affine of the previous block for this thread's 4 A columns, per row segment
-    float sc[2][4], sh[2][4];
-#pragma unroll
-    for (int sg = 0; sg < 2; ++sg)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            sc[sg][i] = 1.f;
-            sh[sg][i] = 0.f;
+    // (named float4s, not arrays: a per-row segment select must stay a v_cndmask)
+    float4 sc0 = make_float4(1.f, 1.f, 1.f, 1.f), sc1 = sc0;
+    float4 sh0 = make_float4(0.f, 0.f, 0.f, 0.f), sh1 = sh0;
+    if (a.prev_mode == 1 || a.prev_mode == 2) {
+        auto aff = [&](int sg, int i, float& scv, float& shv) {
             const int c = gk + i;
             const int so = two ? sg * k : 0;
-            if ((a.prev_mode == 1 || a.prev_mode == 2) && c < k)
-                bn_affine(a.prev_gamma[c], a.prev_beta[c], a.prev_mean[so + c], a.prev_invstd[so + c], sc[sg][i],
-                          sh[sg][i]);
-        }
+            if (c < k) bn_affine(a.prev_gamma[c], a.prev_beta[c], a.prev_mean[so + c], a.prev_invstd[so + c], scv, shv);
+        };
+        aff(0, 0, sc0.x, sh0.x); aff(0, 1, sc0.y, sh0.y); aff(0, 2, sc0.z, sh0.z); aff(0, 3, sc0.w, sh0.w);
+        aff(1, 0, sc1.x, sh1.x); aff(1, 1, sc1.y, sh1.y); aff(1, 2, sc1.z, sh1.z); aff(1, 3, sc1.w, sh1.w);
+    }
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
                   pseed, nullptr, nullptr};
     const float slope = act_slope(a.prev_act);
-    const bool do_bias = a.dbias != nullptr && blockIdx.y == 0;
+    const bool do_bias = a.dbias != nullptr && by == 0;
 
     if (gather) {
         for (int64_t t = tid; t < r_end - r_begin; t += 256) {
@@ -668,12 +695,14 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(rt_linear_bwd_args a
             const bool ok = r < r_end && (!gather || srow[r - r_begin] >= 0);
             const float d4[4] = {dv[p].x, dv[p].y, dv[p].z, dv[p].w};
             const float a4[4] = {av[p].x, av[p].y, av[p].z, av[p].w};
+            const float4 scs = hi_seg ? sc1 : sc0, shs = hi_seg ? sh1 : sh0;
+            const float scv[4] = {scs.x, scs.y, scs.z, scs.w}, shv[4] = {shs.x, shs.y, shs.z, shs.w};
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 dzT[4 * c4 + i][row] = d4[i];
                 bsum[i] += d4[i];
-                const float scv = hi_seg ? sc[1][i] : sc[0][i], shv = hi_seg ? sh[1][i] : sh[0][i];
-                aT[4 * c4 + i][row] = (ok && gk + i < k) ? pro_col<PRO>(pro, slope, r, gk + i, scv, shv, a4[i]) : 0.f;
+                aT[4 * c4 + i][row] =
+                    (ok && gk + i < k) ? pro_col<PRO>(pro, slope, r, gk + i, scv[i], shv[i], a4[i]) : 0.f;
             }
         }
         __syncthreads();
@@ -729,7 +758,7 @@ static void allow_lds(K kernel, size_t bytes) {
     }
 }
 
-extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
+static int validate_fwd(const rt_linear_fwd_args* args) {
     if (!args) return RT_ERR_INVALID;
     const rt_linear_fwd_args& a = *args;
     if (a.m < 0 || a.k <= 0 || a.n <= 0 || !a.src || !a.w || a.ld_src < a.k) return RT_ERR_INVALID;
@@ -739,19 +768,45 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
         return RT_ERR_INVALID;
     if (a.prev_mode == 1 && (!a.prev_stats || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
-    if (a.m == 0) return RT_OK;
-    const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
     const int kp = mlp::pad8(a.k);
-    const size_t lds = (2 * kp + mlp::FM * (kp + 4) + 4 * tpw * mlp::FM) * sizeof(float) +
+    const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
+    const size_t lds = (2 * kp + mlp::FM * (kp + 4) + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
+    if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
+    return RT_OK;
+}
+
+extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_args, void* stream) {
+    if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+    int tpw = 1, kp_max = 0;
+    bool kvec = true;
+    unsigned blocks[2] = {0u, 0u};
+    for (int g = 0; g < n_args; ++g) {
+        const int v = validate_fwd(&args[g]);
+        if (v) return v;
+        const rt_linear_fwd_args& a = args[g];
+        const int t = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
+        tpw = t > tpw ? t : tpw;
+        kvec = kvec && (a.k % 4) == 0 && (reinterpret_cast<uintptr_t>(a.w) & 15) == 0;
+        const int kp = mlp::pad8(a.k);
+        kp_max = kp > kp_max ? kp : kp_max;
+        blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
+    }
+    // LDS carve-up of the kernel built for tpw tiles at the larger k of the two
+    const size_t lds = (2 * kp_max + mlp::FM * (kp_max + 4) + 4 * tpw * mlp::FM) * sizeof(float) +
                        mlp::FM * sizeof(int64_t) + 16;
     if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
-    const bool kvec = (a.k % 4) == 0 && (reinterpret_cast<uintptr_t>(a.w) & 15) == 0;
-    const dim3 grid(static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM));
+    mlp::FwdLaunch L{};
+    L.a0 = args[0];
+    L.a1 = n_args > 1 ? args[1] : args[0];
+    L.split = blocks[0];
+    const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
+    if (total == 0) return RT_OK;
+    const dim3 grid(total);
     hipStream_t st = as_stream(stream);
 #define RT_FWD(T, V)                                                                              \
     do {                                                                                          \
         allow_lds(mlp::linear_fwd_kernel<T, V>, lds);                                             \
-        hipLaunchKernelGGL((mlp::linear_fwd_kernel<T, V>), grid, dim3(256), lds, st, a);          \
+        hipLaunchKernelGGL((mlp::linear_fwd_kernel<T, V>), grid, dim3(256), lds, st, L);          \
     } while (0)
     if (kvec) {
         if (tpw == 1) RT_FWD(1, true); else if (tpw == 2) RT_FWD(2, true); else RT_FWD(4, true);
@@ -760,6 +815,10 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
     }
 #undef RT_FWD
     return check_launch("linear_fwd_kernel");
+}
+
+extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
+    return rt_linear_fwd_f32_multi(args, 1, stream);
 }
 
 static int validate_bwd(const rt_linear_bwd_args* args) {
@@ -782,52 +841,99 @@ static int validate_bwd(const rt_linear_bwd_args* args) {
     return RT_OK;
 }
 
-extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream) {
-    const int v = validate_bwd(args);
-    if (v) return v;
-    const rt_linear_bwd_args& a = *args;
-    if (a.m == 0) return RT_OK;
+extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream) {
+    if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+    int tpwk = 1;
+    size_t lds = 0;
+    unsigned blocks[2] = {0u, 0u};
+    for (int g = 0; g < n_args; ++g) {
+        const int v = validate_bwd(&args[g]);
+        if (v) return v;
+        const rt_linear_bwd_args& a = args[g];
+        const bool need_da = a.g_prev || a.dsrc;
+        const int t = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
+        tpwk = t > tpwk ? t : tpwk;
+        const int np = mlp::pad8(a.n);
+        const size_t l = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) + 16;
+        lds = l > lds ? l : lds;
+        blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
+    }
+    mlp::BwdLaunch L{};
+    L.a0 = args[0];
+    L.a1 = n_args > 1 ? args[1] : args[0];
+    L.split = blocks[0];
+    const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
+    if (total == 0) return RT_OK;
+    const dim3 grid(total);
     hipStream_t st = as_stream(stream);
-    const bool need_da = a.g_prev || a.dsrc;
-    const int tpwk = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
-    const int np = mlp::pad8(a.n);
-    const size_t lds = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) + 16;
-    const dim3 grid(static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM));
     switch (tpwk) {
-        case 1: allow_lds(mlp::linear_bwd_dz_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<1>, grid, dim3(256), lds, st, a); break;
-        case 2: allow_lds(mlp::linear_bwd_dz_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<2>, grid, dim3(256), lds, st, a); break;
-        default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, a); break;
+        case 1: allow_lds(mlp::linear_bwd_dz_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<1>, grid, dim3(256), lds, st, L); break;
+        case 2: allow_lds(mlp::linear_bwd_dz_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<2>, grid, dim3(256), lds, st, L); break;
+        default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, L); break;
     }
     return check_launch("linear_bwd_dz_kernel");
 }
 
-extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream) {
-    const int v = validate_bwd(args);
-    if (v) return v;
-    const rt_linear_bwd_args& a = *args;
-    if (a.m == 0) return RT_OK;
-    hipStream_t st = as_stream(stream);
-    const int tn = (a.n + mlp::DW_T - 1) / mlp::DW_T;
-    const int tk = (a.k + mlp::DW_T - 1) / mlp::DW_T;
-    // ~512 blocks (2 per CU), whole 64-row chunks, <= 32 splits per tile (atomics
-    // per dW element), <= DW_MAXR rows per split (gather ids staged in LDS)
-    int64_t splits = (512 + tn * tk - 1) / (tn * tk);
+extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream) {
+    return rt_linear_bwd_dz_f32_multi(args, 1, stream);
+}
+
+// dW tiling of one Linear: ~512 blocks (2 per CU), whole 64-row chunks, <= 32
+// splits per tile (atomics per dW element), <= DW_MAXR rows per split (gather
+// ids staged in LDS)
+static void dw_plan(const rt_linear_bwd_args& a, unsigned& tn, unsigned& tk, int64_t& splits, int64_t& rps) {
+    tn = static_cast<unsigned>((a.n + mlp::DW_T - 1) / mlp::DW_T);
+    tk = static_cast<unsigned>((a.k + mlp::DW_T - 1) / mlp::DW_T);
+    splits = (512 + tn * tk - 1) / (tn * tk);
     const int64_t max_splits = (a.m + mlp::DW_R - 1) / mlp::DW_R;
     if (splits > max_splits) splits = max_splits;
     if (splits > 32) splits = 32;
     if (splits < 1) splits = 1;
-    int64_t rps = (a.m + splits - 1) / splits;
+    rps = (a.m + splits - 1) / splits;
     rps = (rps + mlp::DW_R - 1) / mlp::DW_R * mlp::DW_R;
     if (a.ids && rps > mlp::DW_MAXR) rps = mlp::DW_MAXR;
     splits = (a.m + rps - 1) / rps;
-    if (splits > 65535) return RT_ERR_UNSUPPORTED;
-    const dim3 grid(static_cast<unsigned>(tn), static_cast<unsigned>(tk), static_cast<unsigned>(splits));
-    int pro = 0;
-    if (a.prev_mode != 0)
-        pro = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
-    const bool vec = (a.n % 4) == 0 && (a.k % 4) == 0 && (a.ld_src % 4) == 0 &&
-                     (reinterpret_cast<uintptr_t>(a.src) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dz_ws) & 15) == 0;
-#define RT_DW(P, V) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<P, V>), grid, dim3(256), 0, st, a, rps)
+}
+
+extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream) {
+    if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+    mlp::BwdLaunch L{};
+    unsigned blocks[2] = {0u, 0u};
+    int pro = -1;
+    bool vec = true;
+    for (int g = 0; g < n_args; ++g) {
+        const int v = validate_bwd(&args[g]);
+        if (v) return v;
+        const rt_linear_bwd_args& a = args[g];
+        unsigned tn = 0, tk = 0;
+        int64_t splits = 0, rps = 0;
+        if (a.m > 0) dw_plan(a, tn, tk, splits, rps);
+        const int64_t nb = static_cast<int64_t>(tn) * tk * splits;
+        if (nb > (1ll << 30)) return RT_ERR_UNSUPPORTED;
+        blocks[g] = static_cast<unsigned>(nb);
+        (g ? L.tn1 : L.tn0) = tn ? tn : 1u;
+        (g ? L.tk1 : L.tk0) = tk ? tk : 1u;
+        (g ? L.rps1 : L.rps0) = rps;
+        int p = 0;
+        if (a.prev_mode != 0) p = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
+        // one kernel for both: prologue 3 ⊇ 2 ⊇ 1 (dropout p = 0 keeps everything);
+        // a raw input (0) and a transformed one cannot share a kernel
+        if (pro >= 0 && (pro == 0) != (p == 0)) {
+            const int r0 = rt_linear_bwd_dw_f32_multi(&args[0], 1, stream);
+            return r0 ? r0 : rt_linear_bwd_dw_f32_multi(&args[1], 1, stream);
+        }
+        pro = p > pro ? p : pro;
+        vec = vec && (a.n % 4) == 0 && (a.k % 4) == 0 && (a.ld_src % 4) == 0 &&
+              (reinterpret_cast<uintptr_t>(a.src) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dz_ws) & 15) == 0;
+    }
+    L.a0 = args[0];
+    L.a1 = n_args > 1 ? args[1] : args[0];
+    L.split = blocks[0];
+    const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
+    if (total == 0) return RT_OK;
+    const dim3 grid(total);
+    hipStream_t st = as_stream(stream);
+#define RT_DW(P, V) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<P, V>), grid, dim3(256), 0, st, L)
     if (vec) {
         switch (pro) { case 0: RT_DW(0, true); break; case 1: RT_DW(1, true); break; case 2: RT_DW(2, true); break; default: RT_DW(3, true); }
     } else {
@@ -835,6 +941,10 @@ extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream
     }
 #undef RT_DW
     return check_launch("linear_bwd_dw_kernel");
+}
+
+extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream) {
+    return rt_linear_bwd_dw_f32_multi(args, 1, stream);
 }
 
 extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {

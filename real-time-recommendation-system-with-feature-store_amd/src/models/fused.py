@@ -11,7 +11,6 @@ accumulated straight into one flat fp32 grad slab (views are the params'
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import itertools
 from dataclasses import dataclass, field
@@ -212,7 +211,47 @@ def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
                   normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
                   stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0) -> ChainCtx:
-    """Run the block chain. ``src`` is the dense input [rows, k0] (fp32) or a
+    """Run the block chain (see ``_forward_plan`` for the arguments)."""
+    ctx, layers = _forward_plan(blocks, src, ids, normalize, seed_offset, stats_arena, seg_split)
+    st = _stream(src)
+    for a in layers:
+        _launch_fwd([a], st)
+    return ctx
+
+
+def chain_forward_pair(first: tuple, second: tuple) -> tuple:
+    """Two independent chains (e.g. the item and the user tower), each given as
+    the ``chain_forward`` positional arguments; layer l of both runs as ONE
+    launch (``rt_linear_fwd_f32_multi``) when the chains have the same depth.
+    Returns the two ChainCtx."""
+    c1, l1 = _forward_plan(*first)
+    c2, l2 = _forward_plan(*second)
+    st = _stream(first[1])
+    if len(l1) == len(l2):
+        for a, b in zip(l1, l2):
+            _launch_fwd([a, b], st)
+    else:
+        for a in l1 + l2:
+            _launch_fwd([a], st)
+    return c1, c2
+
+
+def _launch_fwd(group: list, st) -> None:
+    flops = sum(2.0 * a.m * a.k * a.n for a in group)
+    nbytes = sum(4.0 * (a.m * a.k + a.n * a.k + a.m * a.n) for a in group)
+    with TIMER.region("linear_fwd", flops=flops, bytes_=nbytes):
+        if len(group) == 1:
+            call("rt_linear_fwd_f32", ctypes.byref(group[0]), st)
+        else:
+            arr = (LinearFwdArgs * len(group))(*group)
+            call("rt_linear_fwd_f32_multi", arr, len(group), st)
+
+
+def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
+                  normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
+                  stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0):
+    """Allocate the chain's activations and build its per-layer launch
+    arguments (launched by the callers above). ``src`` is the dense input [rows, k0] (fp32) or a
     feature table when ``ids`` selects its rows (fused gather). ``seg_split`` > 0
     runs two tower calls in one chain: rows [0, seg_split) and [seg_split, m)
     are separate BatchNorm batches (running stats updated in that order)."""
@@ -246,7 +285,7 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
     for wdt in widths:
         stats.append(stats_arena[off:off + n_seg * STAT_SLOTS * 2 * wdt])
         off += n_seg * STAT_SLOTS * 2 * wdt
-    st = _stream(src)
+    layers = []
     cur_src, cur_ids, ld = src, ids, src.shape[1]
     for li, b in enumerate(blocks):
         lin = b.linear
@@ -308,32 +347,65 @@ def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
             else:
                 a.z_out = out.data_ptr()
             ctx.out = out
-        with TIMER.region("linear_fwd", flops=2.0 * m * a.k * a.n, bytes_=4.0 * (m * a.k + a.n * a.k + m * a.n)):
-            call("rt_linear_fwd_f32", ctypes.byref(a), st)
-    return ctx
+        layers.append(a)
+    return ctx, layers
 
 
 def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab: ParamSlab,
                    want_dsrc: bool = False, seed_offset: Optional[torch.Tensor] = None,
-                   stats_arena: Optional[torch.Tensor] = None, attach: bool = True,
-                   dw_stream: Optional[torch.cuda.Stream] = None) -> Optional[torch.Tensor]:
+                   stats_arena: Optional[torch.Tensor] = None, attach: bool = True) -> Optional[torch.Tensor]:
     """Backward through the chain; parameter grads are atomically accumulated
-    into the slab. Returns d src (dense input) when ``want_dsrc``.
+    into the slab. Returns d src (dense input) when ``want_dsrc``."""
+    layers, dsrc, keep = _backward_plan(blocks, ctx, dout, slab, want_dsrc, seed_offset, stats_arena, attach)
+    st = _stream(dout)
+    for a in layers:  # per Linear: dz (+dA) then dW (+dbias), timed separately (bench roofline)
+        _launch_bwd([a], st)
+    return dsrc
 
-    With ``dw_stream`` every layer's dW launch runs on that stream after its dz
-    launch (one event each), overlapping the dz launch of the layer below on
-    the current stream (each layer then keeps its own dz buffer); the current
-    stream joins ``dw_stream`` before returning."""
+
+def chain_backward_pair(first: tuple, second: tuple) -> None:
+    """Backward of two independent chains (``chain_backward`` positional
+    arguments each, no dsrc); layer l of both runs as ONE dz launch and ONE dW
+    launch (``rt_linear_bwd_*_f32_multi``) when the depths match."""
+    # keep1/keep2 hold the planned buffers until every launch is enqueued
+    l1, _, keep1 = _backward_plan(*first)
+    l2, _, keep2 = _backward_plan(*second)
+    st = _stream(first[2])
+    if len(l1) == len(l2):
+        for a, b in zip(l1, l2):
+            _launch_bwd([a, b], st)
+    else:
+        for a in l1 + l2:
+            _launch_bwd([a], st)
+
+
+def _launch_bwd(group: list, st) -> None:
+    da = [a.g_prev is not None or a.dsrc is not None for a in group]
+    flops = sum((2.0 if d else 0.0) * a.m * a.k * a.n for a, d in zip(group, da))
+    nbytes = sum(4.0 * (3 * a.m * a.n + (2 * a.m * a.k if d else 0) + a.n * a.k) for a, d in zip(group, da))
+    arr = (LinearBwdArgs * len(group))(*group)
+    with TIMER.region("linear_bwd_dz", flops=flops, bytes_=nbytes):
+        call("rt_linear_bwd_dz_f32_multi", arr, len(group), st)
+    with TIMER.region("linear_bwd_dw", flops=sum(2.0 * a.m * a.k * a.n for a in group),
+                      bytes_=sum(4.0 * (a.m * a.n + a.m * a.k + a.n * a.k) for a in group)):
+        call("rt_linear_bwd_dw_f32_multi", arr, len(group), st)
+
+
+def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab: ParamSlab,
+                   want_dsrc: bool = False, seed_offset: Optional[torch.Tensor] = None,
+                   stats_arena: Optional[torch.Tensor] = None, attach: bool = True):
+    """Per-Linear backward launch arguments, last layer first, the d src buffer
+    (or None), and the buffers allocated here (the caller keeps them alive until
+    the launches are enqueued, so no later allocation can reuse them early)."""
     dev = dout.device
     dout = dout.contiguous()
     m = ctx.m
     L = len(blocks) - 1
-    st = _stream(dout)
     if attach:
         slab.attach_grads()
     max_w = max(b.linear.out_features for b in blocks)
-    dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev) if dw_stream is None else None
-    keep = []  # per-layer dz buffers read by the dW launches on dw_stream
+    dz_ws = torch.empty((m, max_w), dtype=torch.float32, device=dev)
+    layers = []
     widths = [b.linear.out_features for b in blocks[:-1]]
     n_seg = 2 if ctx.seg_split else 1
     gst_arena = stats_arena if stats_arena is not None else \
@@ -344,6 +416,7 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         off += n_seg * STAT_SLOTS * 2 * wdt
     gs: List[Optional[torch.Tensor]] = [None] * L
     dsrc = torch.empty((m, blocks[0].linear.in_features), dtype=torch.float32, device=dev) if want_dsrc else None
+    keep = [dout, dz_ws, gst_arena]
     for li in range(L, -1, -1):
         b = blocks[li]
         lin = b.linear
@@ -352,11 +425,7 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         a.w = lin.weight.data_ptr()
         a.dw = slab.grad_of(lin.weight).data_ptr()
         a.dbias = slab.grad_of(lin.bias).data_ptr() if lin.bias is not None else None
-        if dw_stream is None:
-            a.dz_ws = dz_ws.data_ptr()
-        else:
-            keep.append(torch.empty((m, lin.out_features), dtype=torch.float32, device=dev))
-            a.dz_ws = keep[-1].data_ptr()
+        a.dz_ws = dz_ws.data_ptr()
         a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
         a.seg_split = ctx.seg_split
         if li == L:
@@ -410,20 +479,7 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
                 a.g_prev_stats = gstats[li - 1].data_ptr()
             g = torch.empty((m, pb.linear.out_features), dtype=torch.float32, device=dev)
             gs[li - 1] = g
+            keep.append(g)
             a.g_prev = g.data_ptr()
-        da = a.g_prev is not None or a.dsrc is not None
-        # two launches, timed separately (bench roofline): dz (+dA) then dW (+dbias)
-        with TIMER.region("linear_bwd_dz", flops=(2.0 if da else 0.0) * m * a.k * a.n,
-                          bytes_=4.0 * (3 * m * a.n + (2 * m * a.k if da else 0) + a.n * a.k)):
-            call("rt_linear_bwd_dz_f32", ctypes.byref(a), st)
-        if dw_stream is not None:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            dw_stream.wait_event(ev)
-        with torch.cuda.stream(dw_stream) if dw_stream is not None else contextlib.nullcontext():
-            with TIMER.region("linear_bwd_dw", flops=2.0 * m * a.k * a.n,
-                              bytes_=4.0 * (m * a.n + m * a.k + a.n * a.k)):
-                call("rt_linear_bwd_dw_f32", ctypes.byref(a), _stream(dout))
-    if dw_stream is not None:
-        torch.cuda.current_stream(dev).wait_stream(dw_stream)
-    return dsrc
+        layers.append(a)
+    return layers, dsrc, keep

@@ -83,6 +83,9 @@ SIGNATURES = {
     "rt_linear_bwd_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_bwd_dz_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_bwd_dw_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
+    "rt_linear_fwd_f32_multi": (c_int, [ctypes.POINTER(LinearFwdArgs), c_int, vp]),
+    "rt_linear_bwd_dz_f32_multi": (c_int, [ctypes.POINTER(LinearBwdArgs), c_int, vp]),
+    "rt_linear_bwd_dw_f32_multi": (c_int, [ctypes.POINTER(LinearBwdArgs), c_int, vp]),
     "rt_twotower_loss_workspace_bytes": (c_size, [c_i64, c_int]),
     "rt_twotower_loss_fwd_bwd": (c_int, [vp, vp, vp, c_int, c_i64, c_int, c_int, c_f32, vp, vp, c_f32,
                                          c_f32, vp, vp, vp, vp, vp, vp, vp, c_size, vp]),

@@ -19,7 +19,8 @@ from typing import Dict, Optional
 import torch
 
 from .. import kernels, native
-from ..models.fused import blocks_from_sequential, chain_backward, chain_forward, stats_arena_size
+from ..models.fused import (blocks_from_sequential, chain_backward, chain_backward_pair, chain_forward,
+                            chain_forward_pair, stats_arena_size)
 from ..models.two_tower import TwoTowerModel
 from ..native import call, ptr
 from ..profiling import TIMER
@@ -122,10 +123,7 @@ class FusedTrainStep:
         so = self.seed_dev
         main = torch.cuda.current_stream(self.dev)
         s_u, s_p = self.side if self.concurrent else (main, main)
-        s_u.wait_stream(main)
-        with torch.cuda.stream(s_u):
-            u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
-        b = u.m
+        b = user_ids.numel() if user_ids is not None else user_src.shape[0]
         # positives and negatives go through the item tower as ONE chain of
         # B + B·N rows whose two row segments are separate BatchNorm batches
         # (the reference's two item-tower calls, src/training/trainers/two_tower.py:
@@ -138,14 +136,20 @@ class FusedTrainStep:
                 item_src, item_ids = pos_src, torch.cat([pos_ids.reshape(-1), neg_ids.reshape(-1)])
             else:
                 item_src, item_ids = torch.cat([pos_src, neg_src]), None
-            pq = chain_forward(ib, item_src, item_ids, seed_offset=so, stats_arena=self.a_pqf, seg_split=b)
+            # user tower and merged item tower: layer l of both in ONE launch
+            pq, u = chain_forward_pair((ib, item_src, item_ids, True, so, self.a_pqf, b),
+                                       (ub, user_src, user_ids, True, so, self.a_uf, 0))
             p_out, q_out = pq.out[:b], pq.out[b:]
         else:
             p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf)
             q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
                 if (neg_src is not None) else None
             p_out, q_out = p.out, (q.out if q is not None else None)
-        main.wait_stream(s_u)
+        if not merged:
+            s_u.wait_stream(main)
+            with torch.cuda.stream(s_u):
+                u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
+            main.wait_stream(s_u)
         d = u.out.shape[1]
         n_neg = (q_out.shape[0] // b) if q_out is not None else 0
         du = torch.empty_like(u.out)
@@ -165,12 +169,13 @@ class FusedTrainStep:
                  ptr(slab.grad_of(ubias)) if ubias is not None else None,
                  ptr(slab.grad_of(ibias)) if ibias is not None else None, ptr(ws), ws.numel(), st)
         # backward: independent chains (grads meet in the slab through atomics)
-        s_u.wait_stream(main)
-        with torch.cuda.stream(s_u):
-            chain_backward(ub, u, du, slab, seed_offset=so, stats_arena=self.a_ub, attach=False)
-        if merged:
-            chain_backward(ib, pq, dpq, slab, seed_offset=so, stats_arena=self.a_pqb, attach=False)
+        if merged:  # user and item tower layer l in one dz and one dW launch
+            chain_backward_pair((ib, pq, dpq, slab, False, so, self.a_pqb, False),
+                                (ub, u, du, slab, False, so, self.a_ub, False))
         else:
+            s_u.wait_stream(main)
+            with torch.cuda.stream(s_u):
+                chain_backward(ub, u, du, slab, seed_offset=so, stats_arena=self.a_ub, attach=False)
             s_p.wait_stream(main)
             with torch.cuda.stream(s_p):
                 chain_backward(ib, p, dp, slab, seed_offset=so, stats_arena=self.a_pb, attach=False)
