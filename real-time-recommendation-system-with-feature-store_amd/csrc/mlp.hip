@@ -38,6 +38,7 @@ struct BwdLaunch {
     unsigned split;
     int64_t rps0, rps1;     // dW: rows per split
     unsigned tn0, tk0, tn1, tk1;  // dW: tile grid of each group
+    bool vec0, vec1;              // dW: float4 staging loads
 };
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
@@ -177,6 +178,48 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
         const int vpr = kp / 4;
         const int total = FM * vpr;
         const bool vec = (a.ld_src % 4) == 0 && (reinterpret_cast<uintptr_t>(a.src) & 15) == 0;
+        if (vec && (a.k % 4) == 0 && (256 % vpr) == 0 && (pro.mode == 0 || act_is_piecewise_linear(pro.act))) {
+            // fast path: 4 fixed columns per thread (BN affine in registers, no
+            // per-element division / LDS reads / act switch), rows strided by 256/vpr
+            const int c = (tid % vpr) * 4, rstep = 256 / vpr;
+            const bool bn = pro.mode == 1 || pro.mode == 2;
+            const float4 sc4 = bn ? *reinterpret_cast<const float4*>(scale + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+            const float4 sh4 = bn ? *reinterpret_cast<const float4*>(shift + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float sl = act_slope(pro.act);
+            const bool drop = pro.drop_p > 0.f;
+            for (int r0 = tid / vpr; r0 < FM; r0 += 8 * rstep) {
+                float4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int r = r0 + u * rstep;
+                    v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (r < FM && c < k) {
+                        const int64_t sr = srow[r];
+                        if (sr >= 0) v[u] = *reinterpret_cast<const float4*>(a.src + sr * a.ld_src + c);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int r = r0 + u * rstep;
+                    if (r >= FM) break;
+                    const int64_t gr = row0 + r;
+                    const bool ok = srow[r] >= 0 && c < k;
+                    auto tf = [&](float x, int cc, float scv, float shv) {
+                        if (pro.mode == 0) return x;
+                        x = act_pwl(sl, x);
+                        if (bn) x = __builtin_fmaf(x, scv, shv);
+                        if (drop) x = dropout_keep(pro.seed, gr, cc, pro.drop_p) ? x * pro.drop_scale : 0.f;
+                        return x;
+                    };
+                    float4 o;
+                    o.x = ok ? tf(v[u].x, c, sc4.x, sh4.x) : 0.f;
+                    o.y = ok ? tf(v[u].y, c + 1, sc4.y, sh4.y) : 0.f;
+                    o.z = ok ? tf(v[u].z, c + 2, sc4.z, sh4.z) : 0.f;
+                    o.w = ok ? tf(v[u].w, c + 3, sc4.w, sh4.w) : 0.f;
+                    *reinterpret_cast<float4*>(As + r * lda + c) = o;
+                }
+            }
+        } else
         for (int base = tid; base < total; base += 256 * 4) {
             float4 v[4];
 #pragma unroll
@@ -412,6 +455,48 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
         const int vpr = np / 4;
         const int total = FM * vpr;
         const bool vec = (n % 4) == 0;
+        if (vec && (256 % vpr) == 0 && act_is_piecewise_linear(a.act) && a.grad_mode != 3) {
+            // fast path: each thread owns 4 fixed columns (coefficients in
+            // registers, no per-element division or LDS reads), rows strided by
+            // 256/vpr; all g/z loads of the thread issued before the math
+            const int c = (tid % vpr) * 4, rstep = 256 / vpr;
+            const float4 fA = *reinterpret_cast<const float4*>(cA + c), fB = *reinterpret_cast<const float4*>(cB + c);
+            const float4 fC = *reinterpret_cast<const float4*>(cC + c), fM = *reinterpret_cast<const float4*>(cM + c);
+            const float4 fI = *reinterpret_cast<const float4*>(cI + c);
+            const float sl = act_slope(a.act);
+            for (int r0 = tid / vpr; r0 < FM; r0 += 8 * rstep) {
+                float4 gv[8], zv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int r = r0 + u * rstep;
+                    const int64_t gr = row0 + r;
+                    gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    zv[u] = gv[u];
+                    if (r < FM && gr < m && c < n) {
+                        gv[u] = *reinterpret_cast<const float4*>(a.g + gr * n + c);
+                        zv[u] = *reinterpret_cast<const float4*>(a.z + gr * n + c);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int r = r0 + u * rstep;
+                    if (r >= FM) break;
+                    const int64_t gr = row0 + r;
+                    auto one = [&](float g, float z, float A, float B, float C, float M, float I) {
+                        const float xh = (act_pwl(sl, z) - M) * I;
+                        return A * (g - B - xh * C) * (z > 0.f ? 1.f : sl);
+                    };
+                    float4 d;
+                    d.x = one(gv[u].x, zv[u].x, fA.x, fB.x, fC.x, fM.x, fI.x);
+                    d.y = one(gv[u].y, zv[u].y, fA.y, fB.y, fC.y, fM.y, fI.y);
+                    d.z = one(gv[u].z, zv[u].z, fA.z, fB.z, fC.z, fM.z, fI.z);
+                    d.w = one(gv[u].w, zv[u].w, fA.w, fB.w, fC.w, fM.w, fI.w);
+                    if (gr >= m || c >= n) d = make_float4(0.f, 0.f, 0.f, 0.f);
+                    *reinterpret_cast<float4*>(Dz + r * ldz + c) = d;
+                    if (gr < m && c < n) *reinterpret_cast<float4*>(a.dz_ws + gr * n + c) = d;
+                }
+            }
+        } else
         for (int base = tid; base < total; base += 256 * 4) {
             float4 gv[4], zv[4];
 #pragma unroll
@@ -577,7 +662,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
 // tiles TRANSPOSED into LDS ([col][row], 16-B aligned rows), so each lane's
 // MFMA operands are contiguous: lane half h reduces rows h·32 + s, and one
 // ds_read_b128 feeds 4 v_mfma_f32_32x32x2_f32 k-steps. The tile is added to
-// dW with one fp32 atomic per element per block (<= 32 splits, see the host).
+// dW with one fp32 atomic per element per block (<= 128 splits, see the host).
 //   PRO: 0 raw A, 1 piecewise-linear act, 2 same + dropout, 3 generic act.
 constexpr int DW_T = 64;          // n and k per block
 constexpr int DW_R = 64;          // rows per chunk
@@ -600,7 +685,7 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
     }
 }
 
-template <int PRO, bool VEC>  // VEC: n, k, ld_src multiples of 4 and 16-B aligned rows
+template <int PRO>
 __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
@@ -609,6 +694,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
     const unsigned tn = g1 ? L.tn1 : L.tn0, tk = g1 ? L.tk1 : L.tk0;
     const unsigned bx = bid % tn, by = (bid / tn) % tk, bz = bid / (tn * tk);
+    const bool vec = g1 ? L.vec1 : L.vec0;  // n, k, ld_src multiples of 4, 16-B aligned rows
     __shared__ __attribute__((aligned(16))) float dzT[DW_T][DW_LD];
     __shared__ __attribute__((aligned(16))) float aT[DW_T][DW_LD];
     __shared__ int srow[DW_MAXR];
@@ -666,7 +752,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
             const float* dz = a.dz_ws + r * n + gn;
             const int64_t sr = gather ? srow[r - r_begin] : r;
             const float* ap = a.src + sr * a.ld_src + gk;
-            if constexpr (VEC) {
+            if (vec) {
                 if (gn < n) dv[p] = *reinterpret_cast<const float4*>(dz);
                 if (gk < k && sr >= 0) av[p] = *reinterpret_cast<const float4*>(ap);
             } else {
@@ -879,15 +965,17 @@ extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream
 }
 
 // dW tiling of one Linear: ~512 blocks (2 per CU), whole 64-row chunks, <= 32
-// splits per tile (atomics per dW element), <= DW_MAXR rows per split (gather
-// ids staged in LDS)
+// splits per tile (atomics per dW element; 128 for <= 4 tiles), <= DW_MAXR
+// rows per split (gather ids staged in LDS)
 static void dw_plan(const rt_linear_bwd_args& a, unsigned& tn, unsigned& tk, int64_t& splits, int64_t& rps) {
     tn = static_cast<unsigned>((a.n + mlp::DW_T - 1) / mlp::DW_T);
     tk = static_cast<unsigned>((a.k + mlp::DW_T - 1) / mlp::DW_T);
     splits = (512 + tn * tk - 1) / (tn * tk);
     const int64_t max_splits = (a.m + mlp::DW_R - 1) / mlp::DW_R;
     if (splits > max_splits) splits = max_splits;
-    if (splits > 32) splits = 32;
+    // measured: 32 splits is best for 8 tiles (layer 2), 128 for 4 (layer 1, k = 20)
+    const int64_t cap = tn * tk <= 4 ? 128 : 32;
+    if (splits > cap) splits = cap;
     if (splits < 1) splits = 1;
     rps = (a.m + splits - 1) / splits;
     rps = (rps + mlp::DW_R - 1) / mlp::DW_R * mlp::DW_R;
@@ -900,7 +988,6 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     mlp::BwdLaunch L{};
     unsigned blocks[2] = {0u, 0u};
     int pro = -1;
-    bool vec = true;
     for (int g = 0; g < n_args; ++g) {
         const int v = validate_bwd(&args[g]);
         if (v) return v;
@@ -923,22 +1010,20 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
             return r0 ? r0 : rt_linear_bwd_dw_f32_multi(&args[1], 1, stream);
         }
         pro = p > pro ? p : pro;
-        vec = vec && (a.n % 4) == 0 && (a.k % 4) == 0 && (a.ld_src % 4) == 0 &&
-              (reinterpret_cast<uintptr_t>(a.src) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dz_ws) & 15) == 0;
+        (g ? L.vec1 : L.vec0) = (a.n % 4) == 0 && (a.k % 4) == 0 && (a.ld_src % 4) == 0 &&
+                                (reinterpret_cast<uintptr_t>(a.src) & 15) == 0 &&
+                                (reinterpret_cast<uintptr_t>(a.dz_ws) & 15) == 0;
     }
     L.a0 = args[0];
     L.a1 = n_args > 1 ? args[1] : args[0];
+    if (n_args == 1) { L.tn1 = L.tn0; L.tk1 = L.tk0; L.rps1 = L.rps0; L.vec1 = L.vec0; }
     L.split = blocks[0];
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
     if (total == 0) return RT_OK;
     const dim3 grid(total);
     hipStream_t st = as_stream(stream);
-#define RT_DW(P, V) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<P, V>), grid, dim3(256), 0, st, L)
-    if (vec) {
-        switch (pro) { case 0: RT_DW(0, true); break; case 1: RT_DW(1, true); break; case 2: RT_DW(2, true); break; default: RT_DW(3, true); }
-    } else {
-        switch (pro) { case 0: RT_DW(0, false); break; case 1: RT_DW(1, false); break; case 2: RT_DW(2, false); break; default: RT_DW(3, false); }
-    }
+#define RT_DW(P) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<P>), grid, dim3(256), 0, st, L)
+    switch (pro) { case 0: RT_DW(0); break; case 1: RT_DW(1); break; case 2: RT_DW(2); break; default: RT_DW(3); }
 #undef RT_DW
     return check_launch("linear_bwd_dw_kernel");
 }

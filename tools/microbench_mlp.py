@@ -97,5 +97,51 @@ def main():
             print(f"bwd m={m:5d} k={k:3d} n={n:3d} {label:14s} {us:8.1f} {fl / us / 1e6:7.2f}")
 
 
+def split_bwd():
+    """dz and dW launches timed separately at the C2 item-tower shapes (17,408
+    rows), hidden-layer form, with and without the dropout prologue."""
+    dev = torch.device("cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    S = 16
+    shapes = [(17408, 128, 128), (17408, 256, 128), (17408, 20, 256)]
+    if "--k" in sys.argv:
+        kk = int(sys.argv[sys.argv.index("--k") + 1])
+        shapes = [t for t in shapes if t[1] == kk]
+    for (m, k, n) in shapes:
+        src = torch.randn(m, k, device=dev)
+        w = torch.randn(n, k, device=dev) * 0.05
+        g = torch.randn(m, n, device=dev)
+        z = torch.randn(m, n, device=dev)
+        dz = torch.empty(m, n, device=dev)
+        dw = torch.zeros(n, k, device=dev)
+        db = torch.zeros(n, device=dev)
+        gst = torch.zeros(2 * S * 2 * n, dtype=torch.float64, device=dev)
+        gprev = torch.empty(m, k, device=dev)
+        gprev_st = torch.zeros(2 * S * 2 * k, dtype=torch.float64, device=dev)
+        one_n, zero_n = torch.ones(2 * n, device=dev), torch.zeros(2 * n, device=dev)
+        one_k, zero_k = torch.ones(2 * k, device=dev), torch.zeros(2 * k, device=dev)
+        for drop in ((0.2,) if "--k" in sys.argv else (0.0, 0.2)):
+            a = LinearBwdArgs()
+            a.m, a.k, a.n, a.w, a.dw, a.dbias, a.dz_ws = m, k, n, w.data_ptr(), dw.data_ptr(), db.data_ptr(), dz.data_ptr()
+            a.grad_mode, a.g, a.z, a.act = 1, g.data_ptr(), z.data_ptr(), 0
+            a.g_stats, a.save_mean, a.save_invstd, a.bn_gamma = gst.data_ptr(), zero_n.data_ptr(), one_n.data_ptr(), one_n.data_ptr()
+            a.dgamma, a.dbeta = zero_n.data_ptr(), zero_n.data_ptr()
+            a.src, a.src_rows, a.ld_src = src.data_ptr(), m, k
+            a.seg_split = 1024
+            if k != 20:
+                a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_seed = 1, 0, drop, 3
+                a.prev_mean, a.prev_invstd = zero_k.data_ptr(), one_k.data_ptr()
+                a.prev_gamma, a.prev_beta = one_k.data_ptr(), zero_k.data_ptr()
+                a.g_prev, a.g_prev_stats = gprev.data_ptr(), gprev_st.data_ptr()
+            t_dz = timeit(lambda: call("rt_linear_bwd_dz_f32", ctypes.byref(a), st))
+            t_dw = timeit(lambda: call("rt_linear_bwd_dw_f32", ctypes.byref(a), st))
+            print(f"m={m} k={k:3d} n={n:3d} drop={drop:.1f}  dz {t_dz:7.1f} us  dw {t_dw:7.1f} us  "
+                  f"(dA {2 * m * k * n / t_dz / 1e6:6.2f} TF/s, dW {2 * m * k * n / t_dw / 1e6:6.2f} TF/s)")
+
+
 if __name__ == "__main__":
-    main()
+    if "--split" in sys.argv:
+        native.lib()
+        split_bwd()
+    else:
+        main()
