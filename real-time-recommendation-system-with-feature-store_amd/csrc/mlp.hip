@@ -404,7 +404,46 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
     const int64_t seg_m = two ? (my_seg == 0 ? a.seg_split : m - a.seg_split) : m;
 
     // ---- phase A: dz tile ----
-    if (a.grad_mode == 0) {
+    const int l4 = n / 4;  // grad_mode 0 fast path: float4 lanes per row (a power of two <= 64)
+    if (a.grad_mode == 0 && (n % 4) == 0 && l4 <= 64 && (l4 & (l4 - 1)) == 0 && np == n) {
+        // F.normalize backward, every load of the wave's 8 rows issued up front:
+        // l4 lanes per row, 64/l4 rows per pass, segmented lane sums for the dots
+        const int rpp = 64 / l4, sub = lane / l4, li = lane % l4, c = 4 * li;
+        float4 lv[8], dv[8];
+        float nr[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int r = w * 8 + p * rpp + sub;
+            const int64_t gr = row0 + r;
+            lv[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            dv[p] = lv[p];
+            nr[p] = 1.f;
+            if (p * rpp < 8 && gr < m) {
+                lv[p] = *reinterpret_cast<const float4*>(a.l2_out + gr * n + c);
+                dv[p] = *reinterpret_cast<const float4*>(a.dout + gr * n + c);
+                nr[p] = a.norms[gr];
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            if (p * rpp >= 8) break;
+            const int r = w * 8 + p * rpp + sub;
+            const int64_t gr = row0 + r;
+            float dot = lv[p].x * dv[p].x + lv[p].y * dv[p].y + lv[p].z * dv[p].z + lv[p].w * dv[p].w;
+            for (int o = 1; o < l4; o <<= 1) dot += __shfl_xor(dot, o, 64);
+            const bool big = nr[p] > kNormEps;
+            const float inv = 1.f / (big ? nr[p] : kNormEps);
+            float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gr < m) {
+                d.x = big ? (dv[p].x - lv[p].x * dot) * inv : dv[p].x * inv;
+                d.y = big ? (dv[p].y - lv[p].y * dot) * inv : dv[p].y * inv;
+                d.z = big ? (dv[p].z - lv[p].z * dot) * inv : dv[p].z * inv;
+                d.w = big ? (dv[p].w - lv[p].w * dot) * inv : dv[p].w * inv;
+                *reinterpret_cast<float4*>(a.dz_ws + gr * n + c) = d;
+            }
+            *reinterpret_cast<float4*>(Dz + r * ldz + c) = d;
+        }
+    } else if (a.grad_mode == 0) {
         for (int rr = w * 8; rr < w * 8 + 8; ++rr) {
             const int64_t gr = row0 + rr;
             if (gr < m) {
