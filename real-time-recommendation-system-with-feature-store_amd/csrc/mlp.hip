@@ -58,7 +58,7 @@ struct Pro {
 
 __device__ __forceinline__ float pro_apply(const Pro& p, int64_t r, int c, float v) {
     if (p.mode == 0) return v;
-    v = act_fwd(p.act, v);
+    v = act_eval(p.act, v);
     if (p.mode != 3) v = __builtin_fmaf(v, p.scale[c], p.shift[c]);
     if (p.drop_p > 0.f) v = dropout_keep(p.seed, r, c, p.drop_p) ? v * p.drop_scale : 0.f;
     return v;
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
             const bool ok = col_ok && gr < m;
             if (ok && a.z_out) a.z_out[gr * n + col] = z;
             if (ok && stats) {
-                const float av = act_fwd(a.act, z);
+                const float av = act_eval(a.act, z);
                 s1 += av;
                 s2 += av * av;
             }
@@ -574,9 +574,9 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
                     const int cc = c + j;
                     float dz = 0.f;
                     if (gr < m && cc < n) {
-                        const float xh = (act_fwd(a.act, zs[j]) - cM[cc]) * cI[cc];
+                        const float xh = (act_eval(a.act, zs[j]) - cM[cc]) * cI[cc];
                         const float dr = (a.grad_mode == 3) ? gs[j] : cA[cc] * (gs[j] - cB[cc] - xh * cC[cc]);
-                        dz = dr * act_bwd(a.act, zs[j]);
+                        dz = dr * act_grad_eval(a.act, zs[j]);
                     }
                     dzv[j] = dz;
                 }
@@ -652,6 +652,11 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
     double* const gps = want_stats ? a.g_prev_stats + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
                                                         bid % RT_STAT_SLOTS) * 2 * k : nullptr;
+    // fast epilogue (the C2 hidden layers): a full row block, g_prev only, a
+    // piecewise-linear previous activation — no per-element predicates, 32-bit
+    // offsets from one base pointer, every z_prev load issued before the math
+    const bool fast = row0 + FM <= m && !a.dsrc && a.g_prev && act_is_piecewise_linear(a.prev_act);
+    const float psl = act_slope(a.prev_act);
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
         const int kk = (w + 4 * i) * 32 + c32;
@@ -659,6 +664,27 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
         float s1 = 0.f, s2 = 0.f;
         float pmean = 0.f, pinv = 0.f;
         if (want_stats && col_ok) { pmean = a.prev_mean[my_seg * k + kk]; pinv = a.prev_invstd[my_seg * k + kk]; }
+        if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform: tile past k
+        if (fast) {
+            const int64_t rb = row0 + 4 * h;
+            const float* zp = a.src + rb * a.ld_src + kk;
+            float* gp = a.g_prev + rb * k + kk;
+            float zv[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) zv[r] = (want_stats && col_ok) ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
+            const bool drop = a.prev_drop_p > 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lr = (r & 3) + 8 * (r >> 2);
+                float gv = acc[i][r];
+                if (drop) gv = dropout_keep(pseed, rb + lr, kk, a.prev_drop_p) ? gv * pscale : 0.f;
+                if (col_ok) gp[lr * k] = gv;
+                const float xh = (act_pwl(psl, zv[r]) - pmean) * pinv;
+                s1 += gv;
+                s2 += gv * xh;
+            }
+            if (!want_stats || !col_ok) s1 = s2 = 0.f;
+        } else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t gr = row0 + (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -671,7 +697,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
                         gv = dropout_keep(pseed, gr, kk, a.prev_drop_p) ? da * pscale : 0.f;
                     a.g_prev[gr * k + kk] = gv;
                     if (want_stats) {
-                        const float xh = (act_fwd(a.prev_act, a.src[gr * a.ld_src + kk]) - pmean) * pinv;
+                        const float xh = (act_eval(a.prev_act, a.src[gr * a.ld_src + kk]) - pmean) * pinv;
                         s1 += gv;
                         s2 += gv * xh;
                     }
@@ -713,7 +739,7 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
     if constexpr (PRO == 0) {
         return v;
     } else {
-        if constexpr (PRO == 3) v = act_fwd(p.act, v);
+        if constexpr (PRO == 3) v = act_eval(p.act, v);
         else v = act_pwl(slope, v);
         v = __builtin_fmaf(v, sc, sh);
         if constexpr (PRO == 2) v = dropout_keep(p.seed, r, c, p.drop_p) ? v * p.drop_scale : 0.f;

@@ -117,6 +117,19 @@ __device__ __forceinline__ float act_bwd(int act, float z) {
     }
 }
 
+// Code-size-aware forms for unrolled hot loops: piecewise-linear activations
+// (ReLU / LeakyReLU / identity) inline as one select, the transcendental ones
+// through an out-of-line call, so dozens of unrolled call sites do not inline
+// erf/tanh/exp bodies (the instruction cache is shared by the CU pair)
+__device__ __noinline__ float act_fwd_call(int act, float z) { return act_fwd(act, z); }
+__device__ __noinline__ float act_bwd_call(int act, float z) { return act_bwd(act, z); }
+__device__ __forceinline__ float act_eval(int act, float z) {
+    return act_is_piecewise_linear(act) ? act_pwl(act_slope(act), z) : act_fwd_call(act, z);
+}
+__device__ __forceinline__ float act_grad_eval(int act, float z) {
+    return act_is_piecewise_linear(act) ? (z > 0.f ? 1.f : act_slope(act)) : act_bwd_call(act, z);
+}
+
 // ---- (score, id) ordering: a better than b ⇔ score desc, then id asc ----
 // ids are carried as uint32 local indices inside kernels; 0xFFFFFFFF = empty.
 __device__ __forceinline__ bool better(float sa, uint32_t ia, float sb, uint32_t ib) {
