@@ -331,6 +331,22 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
         const bool col_ok = col < n;
         const float b = (col_ok && a.bias) ? a.bias[col] : 0.f;
         float s1 = 0.f, s2 = 0.f;
+        if (row0 + FM <= m && a.z_out && !l2 && act_is_piecewise_linear(a.act)) {
+            // full row block (the C2 hidden layers): no per-element predicates,
+            // 32-bit offsets from one base pointer
+            if (ct * 32 >= n) continue;  // wave-uniform
+            float* zp = a.z_out + (row0 + 4 * h) * n + col;
+            const float sl = act_slope(a.act);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float z = acc[i][r] + b;
+                if (col_ok) zp[((r & 3) + 8 * (r >> 2)) * n] = z;
+                const float av = act_pwl(sl, z);
+                s1 += av;
+                s2 += av * av;
+            }
+            if (!col_ok) s1 = s2 = 0.f;
+        } else
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
