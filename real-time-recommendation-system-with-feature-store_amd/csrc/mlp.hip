@@ -736,19 +736,20 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
 // M split over the blocks of a group
 // ---------------------------------------------------------------------------
 // Block = one 64(n) x 64(k) tile of dW over a contiguous row range, 4 waves
-// each owning a 32 x 32 quarter. Rows stream in chunks of 64: every thread
-// loads a float4 of dz and of A for 4 rows (global loads of chunk c+1 are in
+// each owning a 32 x 32 quarter. Rows stream in chunks of 128: every thread
+// loads a float4 of dz and of A for 8 rows (global loads of chunk c+1 are in
 // flight while chunk c is multiplied), applies the A prologue (act → BN
 // affine → dropout, the forward's own transform) on registers and writes both
 // tiles TRANSPOSED into LDS ([col][row], 16-B aligned rows), so each lane's
-// MFMA operands are contiguous: lane half h reduces rows h·32 + s, and one
+// MFMA operands are contiguous: lane half h reduces rows h·64 + s, and one
 // ds_read_b128 feeds 4 v_mfma_f32_32x32x2_f32 k-steps. The tile is added to
 // dW with one fp32 atomic per element per block (<= 128 splits, see the host).
 //   PRO: 0 raw A, 1 piecewise-linear act, 2 same + dropout, 3 generic act.
 constexpr int DW_T = 64;          // n and k per block
-constexpr int DW_R = 64;          // rows per chunk
+constexpr int DW_R = 128;         // rows per chunk
+constexpr int DW_P = DW_R / 16;   // rows per staging thread per chunk
 constexpr int DW_LD = DW_R + 4;   // LDS row stride (floats) of the transposed tiles
-constexpr int DW_MAXR = 4096;     // rows per split whose gather ids are staged in LDS
+constexpr int DW_MAXR = 2048;     // rows per split whose gather ids are staged in LDS
 
 template <int PRO>
 __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, int c, float sc, float sh, float v) {
@@ -785,6 +786,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
     const int n0 = static_cast<int>(bx) * DW_T, k0 = static_cast<int>(by) * DW_T;
     const int64_t r_begin = static_cast<int64_t>(bz) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
+    if (r_begin >= m) return;  // a padding split (block-uniform, before any barrier)
     const bool gather = a.ids != nullptr;
     const bool two = a.seg_split > 0;
 
@@ -818,14 +820,14 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
         __syncthreads();
     }
 
-    float4 dv[4], av[4];  // one chunk's staged values (prefetch registers)
+    float4 dv[DW_P], av[DW_P];  // one chunk's staged values (prefetch registers)
     float bsum[4] = {0.f, 0.f, 0.f, 0.f};
     f32x16 acc = f32x16{};
-    const float* ar = &dzT[(w & 1) * 32 + c32][h * 32];
-    const float* br = &aT[(w >> 1) * 32 + c32][h * 32];
+    const float* ar = &dzT[(w & 1) * 32 + c32][h * (DW_R / 2)];
+    const float* br = &aT[(w >> 1) * 32 + c32][h * (DW_R / 2)];
     auto load = [&](int64_t nx) {  // one chunk's dz / A float4s into registers
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < DW_P; ++p) {
             const int64_t r = nx + rr + 16 * p;
             dv[p] = make_float4(0.f, 0.f, 0.f, 0.f);
             av[p] = dv[p];
@@ -855,7 +857,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
         __syncthreads();  // the previous chunk's MFMA reads are done
         // stage: dz as is, A through the prologue, both transposed into LDS
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
+        for (int p = 0; p < DW_P; ++p) {
             const int row = rr + 16 * p;
             const int64_t r = c0 + row;
             const bool hi_seg = two && r >= a.seg_split;
@@ -876,7 +878,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
         // next chunk's loads fly during this chunk's MFMAs
         if (c0 + DW_R < r_end) load(c0 + DW_R);
 #pragma unroll
-        for (int s = 0; s < 32; s += 4) {
+        for (int s = 0; s < DW_R / 2; s += 4) {
             const float4 x = *reinterpret_cast<const float4*>(ar + s);
             const float4 y = *reinterpret_cast<const float4*>(br + s);
             acc = mfma(x.x, y.x, acc);
@@ -1045,7 +1047,7 @@ extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream
     return rt_linear_bwd_dz_f32_multi(args, 1, stream);
 }
 
-// dW tiling of one Linear: ~512 blocks (2 per CU), whole 64-row chunks, <= 32
+// dW tiling of one Linear: ~512 blocks (2 per CU), whole 128-row chunks, <= 32
 // splits per tile (atomics per dW element; 128 for <= 4 tiles), <= DW_MAXR
 // rows per split (gather ids staged in LDS)
 static void dw_plan(const rt_linear_bwd_args& a, unsigned& tn, unsigned& tk, int64_t& splits, int64_t& rps) {
