@@ -239,8 +239,12 @@ def main():
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the captured step")
+    ap.add_argument("--eager", action="store_true",
+                    help="time eager steps (default: hipGraph replays of the captured step, inputs copied in)")
     args = ap.parse_args()
+    # hipGraph replay on one GPU; eager steps under data parallelism (the RCCL
+    # all-reduce between the two captured halves is not exercised off the box)
+    args.graph = not args.eager and args.gpus == 1
 
     dist, rank, world, dev = dist_setup(args.gpus)
     torch.cuda.set_device(dev)
@@ -274,8 +278,12 @@ def main():
     # from an eager pass right after).
     if args.graph:
         st_ids = tuple(t.clone() for t in batches[0])
-        step.capture(ut, mt, mt, user_ids=st_ids[0], pos_ids=st_ids[1], neg_ids=st_ids[2], warmup=1)
-
+        try:
+            step.capture(ut, mt, mt, user_ids=st_ids[0], pos_ids=st_ids[1], neg_ids=st_ids[2], warmup=1)
+        except RuntimeError as e:  # no graph on this runtime: time eager steps instead
+            log(f"hipGraph capture failed ({e}); timing eager steps")
+            args.graph = False
+    if args.graph:
         def run_timed(i):
             for dst, src in zip(st_ids, batches[i % n_batches]):
                 dst.copy_(src, non_blocking=True)
