@@ -60,6 +60,13 @@ def dist_setup(n_gpus):
     return None, 0, 1, torch.device("cuda", 0)
 
 
+def _batch(dev, u, p, n):
+    """Device ids of one batch; positive and negative item ids share one buffer
+    (negatives right after positives: the item tower reads them as one id list)."""
+    pn = torch.from_numpy(np.concatenate([p.reshape(-1), n.reshape(-1)])).to(dev)
+    return torch.from_numpy(u).to(dev), pn[:p.size].view(p.shape), pn[p.size:].view(n.shape)
+
+
 def c2_setup(dev, rank, n_batches):
     from src.data.movielens import build_batches, feature_tables, synthetic_movielens
     from src.training.utils import create_two_tower_model_for_training
@@ -70,7 +77,7 @@ def c2_setup(dev, rank, n_batches):
     model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
                                                         "dropout_rate": 0.2, "temperature": 0.05})
     tables = (torch.from_numpy(uf).to(dev), torch.from_numpy(mf).to(dev))
-    batches = [tuple(torch.from_numpy(x[i]).to(dev) for x in (bu, bp, bn)) for i in range(n_batches)]
+    batches = [_batch(dev, bu[i], bp[i], bn[i]) for i in range(n_batches)]
     return model, tables, batches, (uf, mf, bu, bp, bn)
 
 
@@ -277,7 +284,9 @@ def main():
     # --graph replays the whole step as a captured hipGraph instead (roofline then
     # from an eager pass right after).
     if args.graph:
-        st_ids = tuple(t.clone() for t in batches[0])
+        b0 = batches[0]
+        st_pn = torch.cat([b0[1].reshape(-1), b0[2].reshape(-1)])  # adjacent static pos/neg ids
+        st_ids = (b0[0].clone(), st_pn[:b0[1].numel()].view(b0[1].shape), st_pn[b0[1].numel():].view(b0[2].shape))
         try:
             step.capture(ut, mt, mt, user_ids=st_ids[0], pos_ids=st_ids[1], neg_ids=st_ids[2], warmup=1)
         except RuntimeError as e:  # no graph on this runtime: time eager steps instead

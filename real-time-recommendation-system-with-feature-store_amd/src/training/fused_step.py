@@ -26,6 +26,16 @@ from ..native import call, ptr
 from ..profiling import TIMER
 
 
+def _adjacent_or_cat(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """[a; b] flattened: a view when b directly follows a in one storage (no
+    copy launch), else torch.cat."""
+    if (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.device == b.device
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()):
+        return torch.as_strided(a, (a.numel() + b.numel(),), (1,))
+    return torch.cat([a.reshape(-1), b.reshape(-1)])
+
+
 class FusedTrainStep:
     def __init__(self, model: TwoTowerModel, lr: float = 1e-3, weight_decay: float = 1e-5, max_norm: float = 1.0,
                  betas=(0.9, 0.999), eps: float = 1e-8, explicit_weight: float = 0.7,
@@ -133,7 +143,7 @@ class FusedTrainStep:
             (pos_ids is None and neg_ids is None))
         if merged:
             if pos_ids is not None:
-                item_src, item_ids = pos_src, torch.cat([pos_ids.reshape(-1), neg_ids.reshape(-1)])
+                item_src, item_ids = pos_src, _adjacent_or_cat(pos_ids, neg_ids)
             else:
                 item_src, item_ids = torch.cat([pos_src, neg_src]), None
             # user tower and merged item tower: layer l of both in ONE launch
