@@ -628,6 +628,9 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
     const float* dp = Dz + c32 * ldz + h * nh;
     // 8 k-steps per iteration (nh % 16 == 0); next iteration's W loaded during this one's MFMAs
     float wv[TPWK][8], wn[TPWK][8];
+    // (the W pointer read once: inside the conditional loads below a field of
+    // the selected launch group was re-loaded from the kernarg segment per load)
+    const float* __restrict__ Wt = a.w;
     auto load_w = [&](int s, float (&dst)[TPWK][8]) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
@@ -636,7 +639,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int nn = h * nh + s + j;
-                dst[i][j] = (on && nn < n) ? a.w[static_cast<int64_t>(nn) * k + kk] : 0.f;
+                dst[i][j] = (on && nn < n) ? Wt[static_cast<int64_t>(nn) * k + kk] : 0.f;
             }
         }
     };
@@ -770,7 +773,7 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
 template <int PRO>
 __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
     const bool g1 = blockIdx.x >= L.split;
-    const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
+    const rt_linear_bwd_args a = g1 ? L.a1 : L.a0;  // by value: fields loaded once
     const int64_t rows_per_split = g1 ? L.rps1 : L.rps0;
     // flattened (n tile, k tile, split) of this block within its group
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
