@@ -1050,17 +1050,19 @@ extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream
     return rt_linear_bwd_dz_f32_multi(args, 1, stream);
 }
 
-// dW tiling of one Linear: ~512 blocks (2 per CU), whole 128-row chunks, <= 32
+// dW tiling of one Linear: ~1024 blocks (4 per CU), whole 128-row chunks, <= 64
 // splits per tile (atomics per dW element; 128 for <= 4 tiles), <= DW_MAXR
 // rows per split (gather ids staged in LDS)
 static void dw_plan(const rt_linear_bwd_args& a, unsigned& tn, unsigned& tk, int64_t& splits, int64_t& rps) {
     tn = static_cast<unsigned>((a.n + mlp::DW_T - 1) / mlp::DW_T);
     tk = static_cast<unsigned>((a.k + mlp::DW_T - 1) / mlp::DW_T);
-    splits = (512 + tn * tk - 1) / (tn * tk);
+    splits = (1024 + tn * tk - 1) / (tn * tk);
     const int64_t max_splits = (a.m + mlp::DW_R - 1) / mlp::DW_R;
     if (splits > max_splits) splits = max_splits;
-    // measured: 32 splits is best for 8 tiles (layer 2), 128 for 4 (layer 1, k = 20)
-    const int64_t cap = tn * tk <= 4 ? 128 : 32;
+    // measured (C2 step A/B, lib/variants): a cap of 64 (→ 46 splits of 3 chunks
+    // at m = 17,408) beats 16/32 (slower by 7 % / 2 %) and 128/256 for 8 tiles
+    // (layer 2); 128 for 4 tiles (layers 1 and 3)
+    const int64_t cap = tn * tk <= 4 ? 128 : 64;
     if (splits > cap) splits = cap;
     if (splits < 1) splits = 1;
     rps = (a.m + splits - 1) / splits;
