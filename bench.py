@@ -68,8 +68,8 @@ def _batch(dev, u, p, n):
 
 
 def c2_setup(dev, rank, n_batches):
-    from src.data.movielens import build_batches, feature_tables, synthetic_movielens
-    from src.training.utils import create_two_tower_model_for_training
+    from rtrec_amd.data.movielens import build_batches, feature_tables, synthetic_movielens
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = synthetic_movielens(seed=0)
     uf, mf = feature_tables(data)
     bu, bp, bn = build_batches(data.train_interactions, data.num_movies, 1024, 16, n_batches, seed=100 + rank)
@@ -85,7 +85,7 @@ def cpu_baseline(host, budget_s=10.0):
     """The oracle's torch-CPU restatement of the reference step (same math as
     src/training/trainers/two_tower.py:98-146) on a bounded sample of C2 batches."""
     from oracle import two_tower as orc
-    from src.training.utils import create_two_tower_model_for_training
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
     uf, mf, bu, bp, bn = host
     threads = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
@@ -114,8 +114,8 @@ def cpu_baseline(host, budget_s=10.0):
 
 
 def topk_extras(dev):
-    from src import kernels
-    from src.profiling import TIMER
+    from rtrec_amd import kernels
+    from rtrec_amd.profiling import TIMER
     out = {}
     g = torch.Generator(device=dev).manual_seed(7)
     # config 3: 6040 x 3416 fp32, k=10
@@ -198,10 +198,10 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
     (emb 128) row-sharded over the ranks (1M/N rows each), 65,536 queries per
     launch scanned by every rank against its shard (k=100), the per-slice
     candidate lists sent to the query owners by one all-to-all, owner merge
-    (src/dist/sharded.py::sharded_topk_owner). Strong scaling (fixed corpus);
+    (rtrec_amd/dist/sharded.py::sharded_topk_owner). Strong scaling (fixed corpus);
     time = max over ranks between barriers."""
-    from src import kernels
-    from src.dist.sharded import shard_range, sharded_topk_owner
+    from rtrec_amd import kernels
+    from rtrec_amd.dist.sharded import shard_range, sharded_topk_owner
     n, d, nq, k = 1_000_000, 128, 65536, 100
     b, c = shard_range(n, world, rank)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -255,9 +255,9 @@ def main():
 
     dist, rank, world, dev = dist_setup(args.gpus)
     torch.cuda.set_device(dev)
-    from src import native
-    from src.profiling import TIMER
-    from src.training.fused_step import FusedTrainStep
+    from rtrec_amd import native
+    from rtrec_amd.profiling import TIMER
+    from rtrec_amd.training.fused_step import FusedTrainStep
     native.lib()
 
     n_batches = min(args.steps + args.warmup, 64)

@@ -7,7 +7,7 @@ identical to the reference (``mlp.{i}``, ``embeddings.*``,
 ``content_projection.*``, ``user_bias``/``item_bias``), so reference
 checkpoints load unchanged. ``forward`` never runs the ``nn.Linear`` /
 ``nn.BatchNorm1d`` modules: each tower is one fused chain of gfx950 launches
-(src.models.fused) and the losses are fused forward+backward kernels
+(rtrec_amd.models.fused) and the losses are fused forward+backward kernels
 (librtrec_hip.so). CPU tensors raise: there is no CPU fallback.
 """
 from __future__ import annotations

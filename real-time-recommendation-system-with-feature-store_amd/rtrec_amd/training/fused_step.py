@@ -262,29 +262,3 @@ class FusedTrainStep:
         self.steps += 1
         return self.loss_buf
 
-
-def smoke_check(dev: torch.device):
-    """Tiny train step vs the CPU oracle (called by __graft_entry__.smoke)."""
-    import numpy as np
-    from oracle import two_tower as orc
-    from ..training.utils import create_two_tower_model_for_training
-    torch.manual_seed(0)
-    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 32, "hidden_layers": [64, 32],
-                                                        "dropout_rate": 0.0, "temperature": 0.05})
-    us = {k: v.clone() for k, v in model.user_tower.state_dict().items()}
-    its = {k: v.clone() for k, v in model.item_tower.state_dict().items()}
-    g = torch.Generator().manual_seed(1)
-    uf = torch.randn(32, 3, generator=g)
-    pf = torch.rand(32, 20, generator=g)
-    nf = torch.rand(32, 4, 20, generator=g)
-    ref = orc.train_step(us, its, {"user_bias": torch.zeros(1), "item_bias": torch.zeros(1)}, {}, uf, pf, nf,
-                         temperature=0.05)
-    model.to(dev)
-    step = FusedTrainStep(model)
-    loss = step(uf.to(dev), pf.to(dev), nf.to(dev))
-    torch.cuda.synchronize()
-    got = float(loss[0].item())
-    assert abs(got - ref["loss"]) <= 1e-4 * abs(ref["loss"]), (got, ref["loss"])
-    w_ref = us["mlp.0.weight"].numpy()
-    w_got = model.user_tower.mlp[0].weight.detach().cpu().numpy()
-    np.testing.assert_allclose(w_got, w_ref, rtol=1e-3, atol=1e-5)

@@ -17,7 +17,7 @@ HEADER = REPO / "include" / "rtrec_hip.h"
 
 @pytest.fixture(scope="module")
 def native():
-    from src import native as nat
+    from rtrec_amd import native as nat
     if not (PKG / "lib" / "librtrec_hip.so").exists():
         subprocess.run(["make", "-s", "-j8", "-C", str(PKG)], check=True)
     nat.lib()
@@ -107,7 +107,7 @@ def test_argument_errors_are_status_codes(native):
 
 
 def test_product_path_refuses_cpu_tensors(native):
-    from src import kernels
+    from rtrec_amd import kernels
     t = torch.zeros(4, 8)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         kernels.gather_rows(t, torch.zeros(2, dtype=torch.int64))

@@ -8,8 +8,8 @@ import pandas as pd
 import pytest
 import torch
 
-from src.data.movielens import MovieLensLoader, build_batches, feature_tables, get_user_positive_items
-from src.training.datasets.movielens import MovieLensDataset, PositiveCSR, collate_fn
+from rtrec_amd.data.movielens import MovieLensLoader, build_batches, feature_tables, get_user_positive_items
+from rtrec_amd.training.datasets.movielens import MovieLensDataset, PositiveCSR, collate_fn
 
 
 @pytest.fixture(scope="module")
@@ -88,7 +88,7 @@ def test_build_batches_sampling_properties():
 
 
 def test_plateau_scheduler_matches_torch():
-    from src.training.trainers.two_tower import _ReduceLROnPlateau
+    from rtrec_amd.training.trainers.two_tower import _ReduceLROnPlateau
 
     class _Step:
         lr = 1e-3

@@ -1,5 +1,5 @@
 """N>1 paths on CPU: world_size-2 gloo process groups driving
-the same orchestration code the GPU ranks run (src/dist/sharded.py), with the
+the same orchestration code the GPU ranks run (rtrec_amd/dist/sharded.py), with the
 per-rank compute bound to the oracle (tests may use the oracle as checker).
 
 * corpus-sharded exact top-K: merged result == one index over the whole corpus,
@@ -19,7 +19,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import flat_ip as orc
-from src.dist.sharded import (allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_inbatch_step,
+from rtrec_amd.dist.sharded import (allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_inbatch_step,
                                sharded_topk, sharded_topk_owner)
 
 

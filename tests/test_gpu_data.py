@@ -10,8 +10,8 @@ import numpy as np
 import pytest
 import torch
 
-from src import kernels
-from src.training.datasets.movielens import DeviceFeeder, PositiveCSR
+from rtrec_amd import kernels
+from rtrec_amd.training.datasets.movielens import DeviceFeeder, PositiveCSR
 
 pytestmark = pytest.mark.gpu
 
@@ -71,7 +71,7 @@ def test_sampler_is_uniform_over_the_pool(device):
 
 
 def _tiny_data():
-    from src.data.movielens import synthetic_movielens
+    from rtrec_amd.data.movielens import synthetic_movielens
     return synthetic_movielens(n_users=300, n_movies=400, n_ratings=20000, seed=3)
 
 
@@ -92,8 +92,8 @@ def test_feeder_batches(device):
 
 
 def test_id_batches_equal_dense_batches(device):
-    from src.training.fused_step import FusedTrainStep
-    from src.training.utils import create_two_tower_model_for_training
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = _tiny_data()
     torch.manual_seed(0)
     m1 = create_two_tower_model_for_training(3, 20, {"embedding_dim": 64, "hidden_layers": [128, 64],
@@ -116,8 +116,8 @@ def test_id_batches_equal_dense_batches(device):
 
 
 def test_trainer_epochs_and_checkpoint(device, tmp_path):
-    from src.training.trainers.two_tower import TwoTowerTrainer
-    from src.training.utils import create_two_tower_model_for_training
+    from rtrec_amd.training.trainers.two_tower import TwoTowerTrainer
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = _tiny_data()
     torch.manual_seed(0)
     model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 64, "hidden_layers": [128, 64]})

@@ -8,8 +8,8 @@ import pytest
 import torch
 
 from oracle import flat_ip as orc
-from src import kernels
-from src.dist.sharded import ShardedFlatIPIndex, shard_range
+from rtrec_amd import kernels
+from rtrec_amd.dist.sharded import ShardedFlatIPIndex, shard_range
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +46,7 @@ def test_shard_then_merge_equals_single_search(device, world, n, k, dtype):
 
 
 def test_sharded_index_single_rank_matches_flat_index(device):
-    from src.serving.retrieval import HipFlatIPIndex
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex
     rng = np.random.default_rng(5)
     corpus = rng.standard_normal((3000, 64)).astype(np.float32)
     queries = rng.standard_normal((40, 64)).astype(np.float32)

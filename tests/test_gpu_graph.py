@@ -11,9 +11,9 @@ pytestmark = pytest.mark.gpu
 
 
 def test_graph_replay_matches_eager(device):
-    from src.data.movielens import build_batches, feature_tables, synthetic_movielens
-    from src.training.fused_step import FusedTrainStep
-    from src.training.utils import create_two_tower_model_for_training
+    from rtrec_amd.data.movielens import build_batches, feature_tables, synthetic_movielens
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = synthetic_movielens(n_users=500, n_movies=600, n_ratings=30000, seed=4)
     uf, mf = feature_tables(data)
     bu, bp, bn = build_batches(data.train_interactions, data.num_movies, 256, 8, 4, seed=9)

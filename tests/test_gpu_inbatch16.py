@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from oracle import two_tower as orc
-from src import kernels
+from rtrec_amd import kernels
 
 pytestmark = pytest.mark.gpu
 

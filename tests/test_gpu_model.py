@@ -19,13 +19,13 @@ RTOL = 1e-4  # north_star: loss/scores within 1e-4 relative
 def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from src import native
+    from rtrec_amd import native
     native.lib()
     return torch.device("cuda:0")
 
 
 def _mods():
-    from src.models.two_tower import ItemTower, TwoTowerModel, UserTower, create_two_tower_model
+    from rtrec_amd.models.two_tower import ItemTower, TwoTowerModel, UserTower, create_two_tower_model
     return UserTower, ItemTower, TwoTowerModel, create_two_tower_model
 
 
@@ -141,8 +141,8 @@ def _flat_state(g, prefix):
 def test_fused_train_step_golden(dev, golden):
     """Two TwoTowerTrainer.train_epoch steps of the reference (C2 architecture,
     dropout 0): loss within 1e-4 rel, parameters after Adam close."""
-    from src.training.fused_step import FusedTrainStep
-    from src.training.utils import create_two_tower_model_for_training
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
     g = golden("train_step_c2")
     model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
                                                         "dropout_rate": 0.0, "temperature": 0.05})

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 def K():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from src import kernels, native
+    from rtrec_amd import kernels, native
     native.lib()
     return kernels
 
@@ -172,7 +172,7 @@ def test_flatip_c3_shape(K):
 
 
 def test_flatip_errors(K):
-    from src.native import RTError
+    from rtrec_amd.native import RTError
     with pytest.raises(RTError):  # fp32 rows must be 16-byte multiples (d % 4 == 0)
         K.flatip_topk(torch.randn(4, 10).cuda(), torch.randn(10, 10).cuda(), 5)
     with pytest.raises(RTError):  # k above the supported maximum
@@ -199,7 +199,7 @@ def test_topk_merge(K):
 
 # ---------------------------------------------------------------- index / engine
 def test_hip_flat_index_semantics(K):
-    from src.serving.retrieval import HipFlatIPIndex, RetrievalEngine
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex, RetrievalEngine
     rng = np.random.default_rng(0)
     emb = rng.standard_normal((1000, 128)).astype(np.float32)
     ids = [f"item_{i}" for i in range(1000)]
@@ -234,7 +234,7 @@ def test_hip_flat_index_semantics(K):
 
 
 def test_index_save_load_roundtrip(K, tmp_path):
-    from src.serving.retrieval import HipFlatIPIndex
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex
     rng = np.random.default_rng(1)
     emb = rng.standard_normal((300, 64)).astype(np.float32)
     idx = HipFlatIPIndex({"dimension": 64})

@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 def K():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from src import kernels, native
+    from rtrec_amd import kernels, native
     native.lib()
     return kernels
 

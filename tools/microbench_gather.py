@@ -10,7 +10,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "real-time-recommendation-system-with-f
 
 import torch  # noqa: E402
 
-from src import kernels  # noqa: E402
+from rtrec_amd import kernels  # noqa: E402
 
 
 def timed(fn, reps=10):

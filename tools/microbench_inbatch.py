@@ -11,7 +11,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "real-time-recommendation-system-with-f
 
 import torch  # noqa: E402
 
-from src import kernels  # noqa: E402
+from rtrec_amd import kernels  # noqa: E402
 
 PEAK = {torch.float32: 157.3e12, torch.float16: 2.5e15, torch.bfloat16: 2.5e15}
 

@@ -14,8 +14,8 @@ sys.path[:0] = [REPO, os.path.join(REPO, "real-time-recommendation-system-with-f
 
 import torch  # noqa: E402
 
-from src import native  # noqa: E402
-from src.native import LinearBwdArgs, LinearFwdArgs, call  # noqa: E402
+from rtrec_amd import native  # noqa: E402
+from rtrec_amd.native import LinearBwdArgs, LinearFwdArgs, call  # noqa: E402
 
 
 def timeit(fn, reps=50):

@@ -9,7 +9,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "real-time-recommendation-system-with-f
 
 import torch  # noqa: E402
 
-from src import kernels  # noqa: E402
+from rtrec_amd import kernels  # noqa: E402
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
