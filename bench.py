@@ -67,7 +67,11 @@ def _batch(dev, u, p, n):
     return torch.from_numpy(u).to(dev), pn[:p.size].view(p.shape), pn[p.size:].view(n.shape)
 
 
-def c2_setup(dev, rank, n_batches):
+def c2_setup(dev, rank, n_batches, dropout=0.2):
+    """The C2 workload: ML-1M-shaped tables resident on the device, id batches
+    (B=1024, N=16), the training-factory model (emb 128, hidden [256,128]).
+    tests/test_gpu_c2_fullsize.py runs this same setup at dropout 0 against
+    the oracle."""
     from rtrec_amd.data.movielens import build_batches, feature_tables, synthetic_movielens
     from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = synthetic_movielens(seed=0)
@@ -75,7 +79,7 @@ def c2_setup(dev, rank, n_batches):
     bu, bp, bn = build_batches(data.train_interactions, data.num_movies, 1024, 16, n_batches, seed=100 + rank)
     torch.manual_seed(1234)
     model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
-                                                        "dropout_rate": 0.2, "temperature": 0.05})
+                                                        "dropout_rate": dropout, "temperature": 0.05})
     tables = (torch.from_numpy(uf).to(dev), torch.from_numpy(mf).to(dev))
     batches = [_batch(dev, bu[i], bp[i], bn[i]) for i in range(n_batches)]
     return model, tables, batches, (uf, mf, bu, bp, bn)

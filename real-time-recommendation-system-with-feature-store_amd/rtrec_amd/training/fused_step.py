@@ -227,18 +227,37 @@ class FusedTrainStep:
 
     # ------------------------------------------------------------------
     # hipGraph capture of the whole step (ids/features in static buffers)
-    def capture(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None, warmup: int = 2):
+    def _state_tensors(self):
+        """Everything a step mutates besides grads/arena: parameters, Adam
+        moments, BN running stats / batch counters, step and dropout counters."""
+        return [self.slab.data, self.exp_avg, self.exp_avg_sq, self.step_dev, self.seed_dev] + \
+            [b for b in self.model.buffers()]
+
+    def capture(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None, warmup: int = 2,
+                restore: bool = True):
         """Capture the step as hipGraph(s) over static inputs (copy new ids /
         features into the tensors passed here, then ``replay()``). With a
         process group the step is two graphs — gradients, then clip+Adam — with
-        the RCCL all-reduce launched eagerly between them."""
+        the RCCL all-reduce launched eagerly between them.
+
+        The ``warmup`` eager steps before capture are real steps on the static
+        inputs (Adam, BN running stats, counters). With ``restore`` (default)
+        the whole training state is snapshotted first and put back afterwards,
+        so the first ``replay()`` is step 1 from the state the caller handed
+        in; ``restore=False`` keeps the warmup updates."""
         self.model.train()
+        snap = [t.clone() for t in self._state_tensors()] if restore else None
         s = torch.cuda.Stream(device=self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._run(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
         torch.cuda.current_stream(self.dev).wait_stream(s)
+        if snap is not None:
+            with torch.no_grad():
+                for t, v in zip(self._state_tensors(), snap):
+                    t.copy_(v)
+            del snap
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._grads(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
@@ -251,7 +270,8 @@ class FusedTrainStep:
             with torch.cuda.graph(g2):
                 self._update()
             self.graph_update = g2
-        self.steps += warmup
+        if not restore:
+            self.steps += warmup
         return g
 
     def replay(self):

@@ -1,0 +1,149 @@
+"""Dropout contract of the fused tower kernels (nn.Dropout(p) in
+[Linear → act → BatchNorm1d → Dropout] blocks, src/models/two_tower.py:60-70).
+
+The mask is a counter-based hash of (seed, row, column) regenerated wherever
+the dropped activation is consumed: the next Linear's forward A staging, the
+dz kernel's g_prev epilogue and the dW kernel's A prologue. The reference's
+torch RNG stream cannot be reproduced, so the contract is checked instead:
+
+* the mask is read back from the forward (a chain whose last Linear is the
+  identity, BN shifted by +1 so no kept value is 0): keep rate 1-p within
+  bounds overall, per column and per row; kept values scaled by exactly
+  1/(1-p); a new mask per call;
+* the backward uses the SAME mask: the fused dW, dbias, dgamma/dbeta and
+  d input equal torch autograd of the same block with that mask applied
+  (fp32, 1e-4 of the gradient's scale), for eval- and train-mode BN.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+M, K0, H, P = 4096, 24, 256, 0.2
+
+
+def _chain(device, bn_train):
+    from rtrec_amd.models.fused import ParamSlab, blocks_from_sequential
+    torch.manual_seed(3)
+    seq = nn.Sequential(nn.Linear(K0, H), nn.ReLU(), nn.BatchNorm1d(H), nn.Dropout(P), nn.Linear(H, H))
+    with torch.no_grad():
+        seq[4].weight.copy_(torch.eye(H))
+        seq[4].bias.zero_()
+        seq[2].bias.fill_(1.0)
+        seq[2].weight.uniform_(0.5, 1.5)
+    seq.to(device).train()
+    if not bn_train:
+        seq[2].eval()
+        with torch.no_grad():
+            seq[2].running_mean.uniform_(-0.1, 0.1)
+            seq[2].running_var.uniform_(0.5, 2.0)
+    slab = ParamSlab(seq).ensure()
+    return seq, blocks_from_sequential(seq), slab
+
+
+def _pre_dropout(seq, x, bn_train, stats=None):
+    """torch fp32 BN(relu(x W1ᵀ + b1)) on the device (autograd-capable)."""
+    z = F.linear(x, seq[0].weight, seq[0].bias)
+    a = F.relu(z)
+    bn = seq[2]
+    if bn_train:
+        return F.batch_norm(a, None, None, bn.weight, bn.bias, training=True, eps=bn.eps)
+    return F.batch_norm(a, bn.running_mean, bn.running_var, bn.weight, bn.bias, training=False, eps=bn.eps)
+
+
+@pytest.mark.parametrize("bn_train", [False, True])
+def test_dropout_mask_rate_scale_and_backward(device, bn_train):
+    from rtrec_amd.models.fused import chain_backward, chain_forward
+    seq, blocks, slab = _chain(device, bn_train)
+    assert blocks[0].drop_p() == P
+    g = torch.Generator(device=device).manual_seed(11)
+    x = torch.randn(M, K0, device=device, generator=g)
+    rm0 = seq[2].running_mean.clone() if bn_train else None
+    ctx = chain_forward(blocks, x, normalize=False)
+    out = ctx.out.clone()
+    torch.cuda.synchronize()
+
+    with torch.no_grad():
+        a = _pre_dropout(seq, x, bn_train)
+    keep = out != 0
+    assert not torch.any((a == 0) & keep)
+    # keep rate: overall (1M elements, sigma 4e-4), per column (4096, sigma 6e-3), per row (256, sigma 2.5e-2)
+    rate = keep.float().mean().item()
+    assert abs(rate - (1 - P)) < 3e-3, rate
+    col = keep.float().mean(0)
+    row = keep.float().mean(1)
+    assert (col - (1 - P)).abs().max().item() < 0.045
+    assert (row - (1 - P)).abs().max().item() < 0.17
+    # no structure: masks of adjacent columns / rows are uncorrelated
+    kf = keep.float() - (1 - P)
+    assert abs((kf[:, 1:] * kf[:, :-1]).mean().item()) < 3e-3
+    assert abs((kf[1:] * kf[:-1]).mean().item()) < 3e-3
+    # kept values are scaled by 1/(1-p) (the identity Linear passes them through exactly)
+    scale = 1.0 / (1.0 - P)
+    want = a * scale
+    torch.testing.assert_close(out[keep], want[keep], rtol=2e-6 if not bn_train else 2e-5, atol=1e-6)
+
+    # backward through the same ctx: grads must use the forward's mask
+    dout = torch.randn(M, H, device=device, generator=g)
+    slab.grad.zero_()
+    dx = chain_backward(blocks, ctx, dout, slab, want_dsrc=True)
+    torch.cuda.synchronize()
+    ref_params = [p.detach().clone().requires_grad_(True) for p in
+                  (seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias, seq[4].weight, seq[4].bias)]
+    xr = x.clone().requires_grad_(True)
+    w1, b1, gam, bet, w2, b2 = ref_params
+    z = F.linear(xr, w1, b1)
+    ar = F.relu(z)
+    if bn_train:
+        ar = F.batch_norm(ar, None, None, gam, bet, training=True, eps=seq[2].eps)
+    else:
+        ar = F.batch_norm(ar, seq[2].running_mean, seq[2].running_var, gam, bet, training=False, eps=seq[2].eps)
+    y = F.linear(ar * keep.float() * scale, w2, b2)
+    (y * dout).sum().backward()
+    got = [seq[0].weight.grad, seq[0].bias.grad, seq[2].weight.grad, seq[2].bias.grad, seq[4].weight.grad,
+           seq[4].bias.grad]
+    names = ["W1", "b1", "gamma", "beta", "W2", "b2"]
+    for name, gg, rp in zip(names, got, ref_params):
+        r = rp.grad
+        tol = 1e-4 * r.abs().max().item() + 1e-7
+        assert (gg - r).abs().max().item() <= tol, (name, (gg - r).abs().max().item(), tol)
+    tol = 1e-4 * xr.grad.abs().max().item() + 1e-7
+    assert (dx - xr.grad).abs().max().item() <= tol
+    if bn_train:  # the running stats moved once (one BN batch)
+        assert not torch.equal(seq[2].running_mean, rm0)
+
+
+def test_dropout_new_mask_per_call(device):
+    from rtrec_amd.models.fused import chain_forward
+    seq, blocks, _ = _chain(device, False)
+    x = torch.randn(M, K0, device=device)
+    m1 = chain_forward(blocks, x, normalize=False).out != 0
+    m2 = chain_forward(blocks, x, normalize=False).out != 0
+    torch.cuda.synchronize()
+    agree = (m1 == m2).float().mean().item()
+    # independent masks agree with probability p^2 + (1-p)^2 = 0.68
+    assert abs(agree - (P * P + (1 - P) ** 2)) < 5e-3, agree
+
+
+def test_fused_step_dropout_seed_advances(device):
+    """The fused step's device dropout counter advances per step, so two steps
+    on the same batch draw different masks (a captured hipGraph included)."""
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
+    torch.manual_seed(0)
+    m = create_two_tower_model_for_training(3, 20, {"embedding_dim": 32, "hidden_layers": [64, 32],
+                                                    "dropout_rate": 0.5, "temperature": 0.05}).to(device)
+    step = FusedTrainStep(m, lr=0.0, weight_decay=0.0)  # lr 0: parameters stay fixed
+    uf = torch.randn(64, 3, device=device)
+    pf = torch.rand(64, 20, device=device)
+    nf = torch.rand(64, 4, 20, device=device)
+    s0 = int(step.seed_dev.item())
+    l1 = step(uf, pf, nf).clone()
+    l2 = step(uf, pf, nf).clone()
+    torch.cuda.synchronize()
+    assert int(step.seed_dev.item()) != s0
+    assert not torch.equal(l1, l2)
+    assert np.isfinite(l1.cpu().numpy()).all() and np.isfinite(l2.cpu().numpy()).all()

@@ -1,7 +1,9 @@
 """hipGraph capture/replay of the fused C2 step (what bench.py times): with
 dropout off, replaying the captured step over fresh ids in the static buffers
 gives the same losses and parameters as the eager step (to the run-to-run
-noise of the fp32/fp64 atomics that accumulate dW and the BN column sums)."""
+noise of the fp32/fp64 atomics that accumulate dW and the BN column sums).
+``capture`` restores the training state its warmup steps touched (default), or
+keeps them (``restore=False``)."""
 import copy
 
 import pytest
@@ -10,9 +12,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_graph_replay_matches_eager(device):
+def _setup(device):
     from rtrec_amd.data.movielens import build_batches, feature_tables, synthetic_movielens
-    from rtrec_amd.training.fused_step import FusedTrainStep
     from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = synthetic_movielens(n_users=500, n_movies=600, n_ratings=30000, seed=4)
     uf, mf = feature_tables(data)
@@ -22,6 +23,39 @@ def test_graph_replay_matches_eager(device):
     torch.manual_seed(0)
     m1 = create_two_tower_model_for_training(3, 20, {"embedding_dim": 64, "hidden_layers": [128, 64],
                                                      "dropout_rate": 0.0, "temperature": 0.05}).to(device)
+    return ut, mt, batches, m1
+
+
+def _check(m1, m2, ref, got):
+    torch.cuda.synchronize()
+    for a, c in zip(ref, got):
+        torch.testing.assert_close(c, a, rtol=1e-6, atol=1e-7)
+    for a, c in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(c, a, rtol=1e-5, atol=1e-6)
+    for a, c in zip(m1.buffers(), m2.buffers()):
+        torch.testing.assert_close(c, a, rtol=1e-5, atol=1e-6)
+
+
+def test_graph_replay_matches_eager(device):
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    ut, mt, batches, m1 = _setup(device)
+    m2 = copy.deepcopy(m1)
+    eager = FusedTrainStep(m1)
+    ref = [eager(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone() for b in batches]
+    g = FusedTrainStep(m2)
+    st = tuple(t.clone() for t in batches[1])
+    g.capture(ut, mt, mt, user_ids=st[0], pos_ids=st[1], neg_ids=st[2], warmup=2)  # state restored
+    got = []
+    for b in batches:
+        for dst, src in zip(st, b):
+            dst.copy_(src)
+        got.append(g.replay().clone())
+    _check(m1, m2, ref, got)
+
+
+def test_graph_capture_keeps_warmup_when_asked(device):
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    ut, mt, batches, m1 = _setup(device)
     m2 = copy.deepcopy(m1)
     eager = FusedTrainStep(m1)
     ref = []
@@ -29,14 +63,10 @@ def test_graph_replay_matches_eager(device):
         ref.append(eager(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone())
     g = FusedTrainStep(m2)
     st = tuple(t.clone() for t in batches[0])
-    g.capture(ut, mt, mt, user_ids=st[0], pos_ids=st[1], neg_ids=st[2], warmup=2)
+    g.capture(ut, mt, mt, user_ids=st[0], pos_ids=st[1], neg_ids=st[2], warmup=2, restore=False)
     got = []
     for b in batches[1:]:
         for dst, src in zip(st, b):
             dst.copy_(src)
         got.append(g.replay().clone())
-    torch.cuda.synchronize()
-    for a, c in zip(ref[2:], got):
-        torch.testing.assert_close(c, a, rtol=1e-6, atol=1e-7)
-    for a, c in zip(m1.parameters(), m2.parameters()):
-        torch.testing.assert_close(c, a, rtol=1e-5, atol=1e-6)
+    _check(m1, m2, ref[2:], got)
