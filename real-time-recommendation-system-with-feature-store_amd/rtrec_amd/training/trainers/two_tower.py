@@ -84,14 +84,24 @@ class TwoTowerTrainer:
                          neg.to(dev) if neg is not None else None)
 
     def train_epoch(self, epoch: int) -> float:
-        """two_tower.py:84-156 (mixed loss when negatives are present, else in-batch only)."""
+        """two_tower.py:84-156 (mixed loss when negatives are present, else in-batch only).
+        Per-batch losses (the reference's tqdm postfix) stay on the device, one
+        fp64 slot per batch; the host reads them once at the end of the epoch
+        (``last_epoch_step_losses``)."""
         self.model.train()
-        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        try:
+            cap = len(self.train_loader)
+        except TypeError:
+            cap = 1024
+        buf = torch.zeros(max(1, cap), dtype=torch.float64, device=self.device)
         n = 0
         for batch in self.train_loader:
-            total += self._run_step(batch)[0]
+            if n == buf.numel():
+                buf = torch.cat([buf, torch.zeros_like(buf)])
+            buf[n:n + 1].copy_(self._run_step(batch)[0:1])
             n += 1
-        avg = float(total.item()) / n if n else 0.0
+        self.last_epoch_step_losses = buf[:n].cpu().numpy()
+        avg = float(self.last_epoch_step_losses.sum()) / n if n else 0.0
         self.train_losses.append(avg)
         return avg
 
