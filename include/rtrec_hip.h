@@ -306,6 +306,46 @@ int rt_clip_adam_step(float* params, const float* grads, float* exp_avg, float* 
                       const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,
                       int step, const int32_t* step_dev, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Offline evaluation (scripts/evaluate_model.py:162-234, src/evaluation/
+ * metrics.py:73-228,248-319).
+ *
+ * rt_exclusion_bitmap: the train-item mask of generate_recommendations
+ *   (evaluate_model.py:224-228: `user_scores[train_item] = -inf` for every
+ *   train item < num_items) as the exclude_bits operand of rt_flatip_topk.
+ *   Row r uses CSR row u = rows ? rows[r] : r (items sorted ascending, unique;
+ *   u outside [0, n_csr_rows) = no exclusions); bits [n_rows, words] uint32,
+ *   words >= ceil(n_items/32), every word written.
+ *
+ * rt_rank_metrics: Evaluator.evaluate per query row r. preds [n_rows,
+ *   list_len] int64 ranked item ids (-1 pads a ragged list); ground truth =
+ *   CSR row gt_rows ? gt_rows[r] : r (sorted unique items; empty = the row is
+ *   skipped, valid[r] = 0, like a user without ground truth); optional
+ *   exclusions (CSR, same indirection) are removed from the list before
+ *   ranking (metrics.py:279-281). k_values: HOST array of n_k ascending
+ *   positive ints, n_k <= RT_METRICS_MAX_K. Predictions must not repeat an item.
+ *   per_row fp64 [n_rows][4*n_k + 2] = recall@k[n_k], precision@k[n_k],
+ *   ndcg@k[n_k], hit_rate@k[n_k], reciprocal rank, average precision
+ *   (the reference's per-user functions, accumulated rank-ascending in fp64).
+ *   coverage_bits (optional, caller-zeroed, ceil(num_items/32) words): items
+ *   of the first max(k) kept predictions of valid rows (metrics.py:287).
+ *
+ * rt_rank_metrics_reduce: out fp64 [n_cols + 2] = mean of each per_row column
+ *   over valid rows (fixed summation order: deterministic), the number of valid
+ *   rows, and coverage = popcount(coverage_bits) / num_items (0 when NULL).
+ * ------------------------------------------------------------------------ */
+#define RT_METRICS_MAX_K 16
+
+int rt_exclusion_bitmap(const int64_t* offsets, const int32_t* items, int64_t n_csr_rows, const int64_t* rows,
+                        int64_t n_rows, int64_t n_items, uint32_t* bits, int64_t words, void* stream);
+int rt_rank_metrics(const int64_t* preds, int64_t n_rows, int list_len, const int64_t* gt_offsets,
+                    const int32_t* gt_items, const int64_t* gt_rows, int64_t n_gt_rows,
+                    const int64_t* ex_offsets, const int32_t* ex_items, const int64_t* ex_rows,
+                    int64_t n_ex_rows, const int32_t* k_values, int n_k, int64_t num_items,
+                    double* per_row, int32_t* valid, uint32_t* coverage_bits, void* stream);
+int rt_rank_metrics_reduce(const double* per_row, const int32_t* valid, int64_t n_rows, int n_cols,
+                           const uint32_t* coverage_bits, int64_t num_items, double* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

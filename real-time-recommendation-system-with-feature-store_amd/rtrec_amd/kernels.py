@@ -154,6 +154,63 @@ def exclusion_bitmap(n_queries: int, n_items: int, excluded, device) -> torch.Te
     return torch.from_numpy(np.ascontiguousarray(packed).view(np.int32).copy()).to(device)
 
 
+def exclusion_bitmap_csr(offsets: torch.Tensor, items: torch.Tensor, n_items: int,
+                         rows: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device exclusion bitmap (rt_exclusion_bitmap): row r masks the items of CSR
+    row ``rows[r]`` (or r) — the train-item -inf mask of generate_recommendations
+    (scripts/evaluate_model.py:224-228). int32 [n_rows, ceil(n_items/32)]."""
+    native.require_device(offsets, items, what="exclusion_bitmap_csr")
+    if offsets.dtype != torch.int64 or items.dtype != torch.int32:
+        raise TypeError("CSR must be int64 offsets and int32 sorted items")
+    n_csr = offsets.numel() - 1
+    if rows is not None:
+        rows = rows.contiguous().to(torch.int64)
+    n_rows = rows.numel() if rows is not None else n_csr
+    words = (n_items + 31) // 32
+    if out is None:
+        out = torch.empty((n_rows, words), dtype=torch.int32, device=offsets.device)
+    call("rt_exclusion_bitmap", ptr(offsets), ptr(items), n_csr, ptr(rows), n_rows, n_items, ptr(out), words,
+         stream_of(offsets))
+    return out
+
+
+def rank_metrics(preds: torch.Tensor, gt_offsets: torch.Tensor, gt_items: torch.Tensor, k_values,
+                 gt_rows: Optional[torch.Tensor] = None, ex_offsets: Optional[torch.Tensor] = None,
+                 ex_items: Optional[torch.Tensor] = None, ex_rows: Optional[torch.Tensor] = None,
+                 num_items: int = 0):
+    """Ranking metrics of Evaluator.evaluate (src/evaluation/metrics.py:248-319) on
+    the device (rt_rank_metrics + rt_rank_metrics_reduce). Returns (per_row fp64
+    [n, 4·n_k+2], valid int32 [n], summary fp64 [4·n_k+4] = column means over
+    valid rows, n_valid, coverage)."""
+    native.require_device(preds, gt_offsets, gt_items, what="rank_metrics")
+    preds = preds.contiguous().to(torch.int64)
+    if preds.dim() != 2:
+        raise ValueError("preds must be [n_rows, list_len]")
+    ks = [int(k) for k in k_values]
+    if not ks or len(ks) > native.RT_METRICS_MAX_K or sorted(set(ks)) != ks or ks[0] <= 0:
+        raise ValueError(f"k_values must be 1..{native.RT_METRICS_MAX_K} ascending positive ints")
+    for t, dt in ((gt_offsets, torch.int64), (gt_items, torch.int32), (ex_offsets, torch.int64),
+                  (ex_items, torch.int32)):
+        if t is not None and t.dtype != dt:
+            raise TypeError("CSR must be int64 offsets and int32 sorted items")
+    n, L = preds.shape
+    nk = len(ks)
+    dev = preds.device
+    per_row = torch.empty((n, 4 * nk + 2), dtype=torch.float64, device=dev)
+    valid = torch.empty(n, dtype=torch.int32, device=dev)
+    cov = torch.zeros((num_items + 31) // 32, dtype=torch.int32, device=dev) if num_items > 0 else None
+    karr = (ctypes.c_int32 * nk)(*ks)
+    st = stream_of(preds)
+    rows = lambda t: None if t is None else t.contiguous().to(torch.int64)  # noqa: E731
+    gt_rows, ex_rows = rows(gt_rows), rows(ex_rows)
+    call("rt_rank_metrics", ptr(preds), n, L, ptr(gt_offsets), ptr(gt_items), ptr(gt_rows), gt_offsets.numel() - 1,
+         ptr(ex_offsets), ptr(ex_items), ptr(ex_rows), (ex_offsets.numel() - 1) if ex_offsets is not None else 0,
+         karr, nk, num_items, ptr(per_row), ptr(valid), ptr(cov), st)
+    summary = torch.empty(4 * nk + 4, dtype=torch.float64, device=dev)
+    call("rt_rank_metrics_reduce", ptr(per_row), ptr(valid), n, 4 * nk + 2, ptr(cov), num_items, ptr(summary), st)
+    return per_row, valid, summary
+
+
 def sample_negatives(pos_offsets: torch.Tensor, pos_items: torch.Tensor, users: torch.Tensor, num_items: int,
                      num_neg: int, seed: int, seed_offset: Optional[torch.Tensor] = None,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:

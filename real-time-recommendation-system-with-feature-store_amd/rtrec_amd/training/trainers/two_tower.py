@@ -143,6 +143,32 @@ class TwoTowerTrainer:
         if is_best:
             torch.save(ckpt, self.checkpoint_dir / "two_tower_best.pth")
 
+    def load_checkpoint(self, path) -> int:
+        """Resume from a checkpoint written by ``save_checkpoint`` here or by the
+        reference's (src/training/trainers/two_tower.py:190-215; same keys,
+        torch.optim.Adam state layout): tower states, biases, Adam moments and
+        step, learning rate, loss history. Loaded with ``weights_only=True``.
+        Returns the checkpoint's epoch. (The reference has no resume path; this
+        is the inverse of its save_checkpoint.)"""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        m = self.model
+        m.user_tower.load_state_dict(ck["user_tower_state"])
+        m.item_tower.load_state_dict(ck["item_tower_state"])
+        m.temperature = ck.get("temperature", m.temperature)
+        with torch.no_grad():
+            for name in ("user_bias", "item_bias"):
+                v = ck.get(name)
+                p = getattr(m, name)
+                if v is not None and p is not None:
+                    p.copy_(torch.as_tensor(v).reshape(p.shape))
+        if ck.get("optimizer_state") is not None:
+            self.step.load_optimizer_state_dict(ck["optimizer_state"])
+        self.train_losses = list(ck.get("train_losses", []))
+        self.val_losses = list(ck.get("val_losses", []))
+        if self.val_losses:
+            self.best_val_loss = min(self.val_losses)
+        return int(ck.get("epoch", 0))
+
     def train(self, num_epochs: int) -> None:
         """two_tower.py:217-262."""
         for epoch in range(1, num_epochs + 1):

@@ -113,3 +113,13 @@ def test_product_path_refuses_cpu_tensors(native):
         kernels.gather_rows(t, torch.zeros(2, dtype=torch.int64))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         kernels.flatip_topk(t, t, 2)
+
+
+def test_ctypes_argument_counts_match_header(native):
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    protos = re.findall(r"^\s*(?:const\s+char\s*\*|int|size_t)\s+(rt_\w+)\s*\(([^;]*?)\)\s*;", text, flags=re.M | re.S)
+    assert protos
+    for name, params in protos:
+        params = params.strip()
+        n = 0 if params in ("", "void") else params.count(",") + 1
+        assert len(native.SIGNATURES[name][1]) == n, (name, n, len(native.SIGNATURES[name][1]))

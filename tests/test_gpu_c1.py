@@ -72,3 +72,30 @@ def test_c1_one_epoch_vs_oracle(device, tmp_path):
     assert early.max() <= 1e-4, early
     assert gap <= 1e-3, gap
     assert abs(res["train_losses"][0] - got.mean()) <= 1e-9 * abs(got.mean())
+
+
+@pytest.mark.timeout(300)
+def test_c1_train_then_evaluate_cli(device, tmp_path):
+    """train_movielens → evaluate_model, the reference's two-script workflow
+    (scripts/train_movielens.py then scripts/evaluate_model.py), end to end on
+    the device: a short training run, then masked top-100 + metrics for every
+    test user; the metrics equal the oracle's on the same recommendation lists."""
+    from oracle import metrics as om
+    from rtrec_amd import evaluate_model as em
+    from rtrec_amd import train_movielens as tm
+    tm.run(tm.build_parser().parse_args([
+        "--synthetic", "--epochs", "1", "--batch-size", "256", "--embedding-dim", "64", "--max-batches", "50",
+        "--checkpoint-dir", str(tmp_path / "ckpt"), "--output-dir", str(tmp_path / "out")]))
+    res = em.run(em.build_parser().parse_args([
+        "--synthetic", "--checkpoint", str(tmp_path / "ckpt" / "two_tower_best.pth"),
+        "--output", str(tmp_path / "results.json")]))
+    r = json.loads((tmp_path / "results.json").read_text())
+    assert r["num_test_users"] > 1000 and 0.0 <= r["recall@10"] <= 1.0
+    data, _ = tm.load_data(tm.build_parser().parse_args(["--synthetic"]))
+    train_items, gt, _, mf = em.prepare_evaluation_data(data)
+    recs = res["recommendations"]
+    assert all(len(v) == 100 and not (set(v) & set(train_items.get(u, []))) for u, v in recs.items())
+    ref = om.evaluate(recs, gt, [5, 10, 20, 50, 100], num_items=mf.shape[0],
+                      exclude_items={u: set(v) for u, v in train_items.items()})
+    for key in ("recall@10", "ndcg@10", "hit_rate@10", "mrr", "map", "coverage", "precision@100"):
+        np.testing.assert_allclose(r[key], ref[key], rtol=1e-12, err_msg=key)

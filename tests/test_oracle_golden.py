@@ -182,3 +182,49 @@ def test_topk_merge_matches_single_search(golden):
     ms, mi = flat_ip.topk_merge(np.stack(parts_s), np.stack(parts_i), 100)
     assert np.array_equal(mi, g["k100_ids"])
     assert np.array_equal(ms, g["k100_scores"])
+
+
+# ---------------------------------------------------------------------------
+# ranking metrics (src/evaluation/metrics.py) — oracle pinned by the reference's
+# own known answers and by its Evaluator output (eval_metrics.npz)
+# ---------------------------------------------------------------------------
+def test_metrics_oracle_known_answers():
+    import math
+    from oracle import metrics as om
+    from _metric_cases import CASES, EVALUATOR, NDCG_REVERSED
+    for fn, pred, gt, k, want in CASES:
+        f = getattr(om, fn)
+        got = f(pred, gt, k) if k is not None else f(pred, gt)
+        assert math.isclose(got, want, rel_tol=1e-12, abs_tol=0.0), (fn, pred, gt, k, got, want)
+    p, g, k = NDCG_REVERSED
+    assert 0.0 < om.ndcg_at_k(p, g, k) < 1.0
+    for preds, gts, ex, ks, ni, want in EVALUATOR:
+        out = om.evaluate(preds, gts, ks, num_items=ni, exclude_items=ex)
+        for key, v in want.items():
+            assert math.isclose(out[key], v, rel_tol=1e-12), (key, out[key], v)
+
+
+def _eval_metrics_inputs(g):
+    users = [int(u) for u in g["test_users"]]
+    preds = {u: [int(x) for x in g["recs"][r]] for r, u in enumerate(users)}
+    for u in range(1000, 1010):
+        preds[u] = list(range(100))
+    gt = {u: set(int(x) for x in g["ground_truth"][r] if x >= 0) for r, u in enumerate(users)}
+    ex = {u: set(int(x) for x in g["exclude"][r] if x >= 0) for r, u in enumerate(users)}
+    preds2 = {u: [int(x) for x in g["preds_with_excluded"][r] if x >= 0] for r, u in enumerate(users)}
+    return preds, preds2, gt, ex
+
+
+def test_metrics_oracle_vs_reference_evaluator(golden):
+    from oracle import metrics as om
+    g = golden("eval_metrics")
+    preds, preds2, gt, ex = _eval_metrics_inputs(g)
+    ks = [int(k) for k in g["k_values"]]
+    for tag, p in (("plain", preds), ("filtered", preds2)):
+        out = om.evaluate(p, gt, ks, num_items=int(g["num_items"]), exclude_items=ex)
+        for key in [f"{m}@{k}" for m in ("recall", "precision", "ndcg", "hit_rate") for k in ks] + \
+                ["mrr", "map", "coverage"]:
+            np.testing.assert_allclose(out[key], g[f"{tag}/{key}"], rtol=1e-13, err_msg=f"{tag} {key}")
+        for k in ks:
+            np.testing.assert_allclose(out[f"per_user_recall@{k}"], g[f"{tag}/per_user_recall@{k}"], rtol=1e-13)
+            np.testing.assert_allclose(out[f"per_user_ndcg@{k}"], g[f"{tag}/per_user_ndcg@{k}"], rtol=1e-13)

@@ -254,6 +254,104 @@ def gen_reference(ref: Path, out: Path):
     _save(out, "param_counts", **{k: np.int64(v) for k, v in counts.items()})
 
 
+def gen_reference_r2(ref: Path, out: Path):
+    """Round-2 fixtures: the reference Evaluator on the eval_topk recommendations,
+    and checkpoints written by the reference's own save_model / save_checkpoint."""
+    sys.path.insert(0, str(HERE / "loguru_stub"))
+    sys.path.insert(0, str(ref))
+    from src.training.utils import create_two_tower_model_for_training  # noqa: E402
+    from src.training.trainers.two_tower import TwoTowerTrainer  # noqa: E402
+    from src.evaluation.metrics import Evaluator  # noqa: E402
+
+    print("reference Evaluator.evaluate on the eval_topk recommendations")
+    with np.load(out / "eval_topk.npz", allow_pickle=False) as z:
+        recs, test_users, excl = z["recs"], z["test_users"], z["exclude"]
+    rng = np.random.default_rng(21)
+    n_items = 400
+    preds, gt, ex = {}, {}, {}
+    for r, u in enumerate(test_users.tolist()):
+        u = int(u)
+        train = set(int(x) for x in excl[r] if x >= 0)
+        pool = np.array(sorted(set(range(n_items)) - train))
+        # ground truth: a few of the top recommendations plus random held-out items
+        n_gt = int(rng.integers(0, 12))
+        picks = set(rng.choice(pool, n_gt, replace=False).tolist()) if n_gt else set()
+        if rng.random() < 0.5:
+            picks |= set(int(x) for x in recs[r, rng.integers(0, 100, 3)])
+        gt[u] = picks
+        preds[u] = [int(x) for x in recs[r]]
+        ex[u] = train
+    # users present in predictions but not in the ground truth are skipped by the Evaluator
+    for u in range(1000, 1010):
+        preds[u] = list(range(100))
+    ev = Evaluator(k_values=[5, 10, 20, 50, 100], num_items=n_items)
+    m = ev.evaluate(preds, gt, ex)
+    # a second run where predictions contain excluded items (the Evaluator's filter shifts ranks)
+    preds2 = {u: (sorted(ex[u])[:5] + p) for u, p in preds.items() if u in ex}
+    m2 = ev.evaluate(preds2, gt, ex)
+    gt_arr = np.full((len(test_users), 20), -1, np.int64)
+    for r, u in enumerate(test_users.tolist()):
+        g = sorted(gt[int(u)])
+        gt_arr[r, :len(g)] = g
+    p2 = np.full((len(test_users), 105), -1, np.int64)
+    for r, u in enumerate(test_users.tolist()):
+        row = preds2[int(u)]
+        p2[r, :len(row)] = row
+
+    def flat(mm, tag):
+        d = {f"{tag}/{k}": np.float64(v) for k, v in mm.to_dict().items()}
+        for k in mm.per_user_recall:
+            d[f"{tag}/per_user_recall@{k}"] = np.asarray(mm.per_user_recall[k], np.float64)
+            d[f"{tag}/per_user_ndcg@{k}"] = np.asarray(mm.per_user_ndcg[k], np.float64)
+        return d
+    _save(out, "eval_metrics", test_users=test_users, recs=recs, exclude=excl, ground_truth=gt_arr,
+          preds_with_excluded=p2, k_values=np.array([5, 10, 20, 50, 100], np.int64), num_items=np.int64(n_items),
+          **flat(m, "plain"), **flat(m2, "filtered"))
+
+    print("reference checkpoints (save_model, TwoTowerTrainer.save_checkpoint)")
+    torch.manual_seed(31)
+    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 64, "hidden_layers": [128, 64],
+                                                        "dropout_rate": 0.0, "temperature": 0.05})
+    g = torch.Generator().manual_seed(32)
+    batches = []
+    for _ in range(2):
+        bsz, nneg = 64, 8
+        uf = torch.randn(bsz, 3, generator=g)
+        pf = (torch.rand(bsz, 20, generator=g) < 0.15).float()
+        pf[:, 18:] = torch.rand(bsz, 2, generator=g)
+        nf = (torch.rand(bsz, nneg, 20, generator=g) < 0.15).float()
+        nf[:, :, 18:] = torch.rand(bsz, nneg, 2, generator=g)
+        batches.append({"user_features": uf, "pos_item_features": pf, "neg_item_features": nf})
+    with tempfile.TemporaryDirectory() as td:
+        trainer = TwoTowerTrainer(model, [batches[0]], [batches[0]],
+                                  {"learning_rate": 1e-3, "weight_decay": 1e-5, "checkpoint_dir": td})
+        trainer.train_epoch(1)
+        trainer.save_checkpoint(1, is_best=True)
+        ck_bytes = (Path(td) / "two_tower_best.pth").read_bytes()
+        model.save_model(str(Path(td) / "model.pth"))
+        sm_bytes = (Path(td) / "model.pth").read_bytes()
+        # what the reference model computes from these weights (eval mode)
+        model.eval()
+        q_u = torch.randn(32, 3, generator=g)
+        q_i = (torch.rand(48, 20, generator=g) < 0.15).float()
+        q_i[:, 18:] = torch.rand(48, 2, generator=g)
+        with torch.no_grad():
+            ue = model.get_user_embeddings({"numerical": q_u, "categorical": {}})
+            ie = model.get_item_embeddings({"numerical": q_i, "categorical": {}})
+        # the step after the checkpoint, continued by the same reference optimizer
+        model.train()
+        trainer.train_loader = [batches[1]]
+        trainer.train_epoch(2)
+        after = {**_state_arrays("after_user", model.user_tower), **_state_arrays("after_item", model.item_tower)}
+    (out / "ckpt_ref_trainer.pth").write_bytes(ck_bytes)
+    (out / "ckpt_ref_model.pth").write_bytes(sm_bytes)
+    print(f"  wrote ckpt_ref_trainer.pth ({len(ck_bytes) / 1024:.1f} KiB), ckpt_ref_model.pth "
+          f"({len(sm_bytes) / 1024:.1f} KiB)")
+    _save(out, "ckpt_ref_expect", q_user=q_u, q_item=q_i, user_emb=ue, item_emb=ie,
+          losses=np.array(trainer.train_losses, np.float64), **after,
+          **{f"b1_{k}": v for k, v in batches[1].items()})
+
+
 def _dyadic_unit(rng, n, d, nnz=16):
     """Unit-norm rows with `nnz` entries of ±1/4 (nnz=16): the renorm is exactly
     the identity and every inner product is an exact multiple of 1/16."""
@@ -320,7 +418,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=str(HERE.parent / "tests" / "golden"))
-    ap.add_argument("--only", choices=["reference", "dyadic"], default=None)
+    ap.add_argument("--only", choices=["reference", "dyadic", "r2"], default=None)
     a = ap.parse_args()
     out = Path(a.out)
     if a.only in (None, "dyadic"):
@@ -331,6 +429,10 @@ def main():
             print(f"reference not found at {ref}; skipping reference vectors")
             return
         gen_reference(ref, out)
+    if a.only in (None, "reference", "r2"):
+        ref = Path(a.ref)
+        if (ref / "src" / "models" / "two_tower.py").exists():
+            gen_reference_r2(ref, out)
 
 
 if __name__ == "__main__":
