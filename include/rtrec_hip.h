@@ -77,7 +77,7 @@ int rt_l2_renorm_f32(float* x, int64_t n, int d, void* stream);
  * src/serving/retrieval.py:96-98,171; and the masked np.dot + argsort of
  * scripts/evaluate_model.py:217-232).
  * queries [nq, d], items [nx, d], both `dtype`, rows 16-byte aligned:
- * f32: d % 4 == 0, d <= 128; f16/bf16: d % 8 == 0, d <= 256; 1 <= k <= 512;
+ * f32: d % 4 == 0, d <= 256; f16/bf16: d % 8 == 0, d <= 256; 1 <= k <= 512;
  * nx + id_offset < 2^32 - 1.
  * exclude_bits: optional uint32 bitmap [nq, exclude_words]; bit j of row q set
  *   means item j is skipped for query q.
@@ -91,6 +91,19 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
                    int k, const uint32_t* exclude_bits, int64_t exclude_words, int64_t id_offset,
                    float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes,
                    void* stream);
+
+/* IndexFlatL2 mode (FaissIndex with metric != "cosine", src/serving/retrieval.py:
+ * 96-100). rt_l2_augment_f32 writes rows [x, a, 0...] of ld_out >= d + 1 floats:
+ * a = 1 for queries (role 0), a = -0.5*||x||^2 for items (role 1); then
+ * rt_flatip_topk on the augmented rows (d' = ld_out) ranks items by
+ * q.x - ||x||^2/2, i.e. by ascending ||q - x||^2. rt_l2_finish_f32 rewrites each
+ * [nq, k] result row (ids = item index + id_offset into x_aug) with Faiss's
+ * reported distance (||q||^2 + ||x||^2 - 2 q.x over the first d columns,
+ * sequential fmaf norms and dot, clamped at 0) re-sorted by (distance asc, id
+ * asc); unfilled slots (FLT_MAX, -1). k <= 512. */
+int rt_l2_augment_f32(const float* x, int64_t n, int d, float* out, int ld_out, int role, void* stream);
+int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq, int k,
+                     float* scores, int64_t* ids, int64_t id_offset, void* stream);
 
 /* Merge n_lists candidate lists per query, layout [n_lists][nq][k_in] (as an
  * all_gather_into_tensor over ranks produces), into the (score desc, id asc)

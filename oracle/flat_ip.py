@@ -44,6 +44,10 @@ def lib():
             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
             ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib.orc_topk_merge.restype = ctypes.c_int
+        _lib.orc_flatl2_search.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int]
+        _lib.orc_flatl2_search.restype = ctypes.c_int
     return _lib
 
 
@@ -83,6 +87,21 @@ def flat_ip_search(queries: np.ndarray, items: np.ndarray, k: int,
                                  _ptr(out_s), _ptr(out_i), nthreads)
     if rc != 0:
         raise RuntimeError(f"orc_flatip_search failed: {rc}")
+    return out_s, out_i
+
+
+def flat_l2_search(queries: np.ndarray, items: np.ndarray, k: int, nthreads: int = 1
+                   ) -> Tuple[np.ndarray, np.ndarray]:
+    """IndexFlatL2 search (retrieval.py:99-100, metric != "cosine"): squared L2
+    distances ascending, ties by id ascending; unfilled = (FLT_MAX, -1)."""
+    q = np.ascontiguousarray(queries, dtype=np.float32)
+    x = np.ascontiguousarray(items, dtype=np.float32)
+    nq, d = q.shape
+    out_s = np.empty((nq, k), np.float32)
+    out_i = np.empty((nq, k), np.int64)
+    rc = lib().orc_flatl2_search(_ptr(q), nq, _ptr(x), x.shape[0], d, k, _ptr(out_s), _ptr(out_i), nthreads)
+    if rc != 0:
+        raise RuntimeError(f"orc_flatl2_search failed: {rc}")
     return out_s, out_i
 
 

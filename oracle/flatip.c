@@ -181,6 +181,53 @@ int orc_flatip_search(const void* Q, int64_t nq, const void* X, int64_t nx, int 
 }
 
 /*
+ * IndexFlatL2.search (src/serving/retrieval.py:99-100, metric != "cosine"):
+ * Faiss's BLAS-path distance ||q||^2 + ||x||^2 - 2 q.x (exhaustive_L2sqr_blas,
+ * clamped at 0), norms and dot as sequential fmaf chains; the k smallest by
+ * (distance asc, id asc) — Faiss's max-heap admits only strictly smaller
+ * distances, so the lower id wins exact ties; unfilled slots (FLT_MAX, -1).
+ * Q [nq, d], X [nx, d] f32.
+ */
+int orc_flatl2_search(const float* Q, int64_t nq, const float* X, int64_t nx, int d, int k,
+                      float* out_s, int64_t* out_i, int nthreads) {
+    if (k <= 0 || d <= 0 || nq < 0 || nx < 0) return -1;
+    float* xn = (float*)malloc((size_t)(nx > 0 ? nx : 1) * 4);
+    if (!xn) return -2;
+    for (int64_t x = 0; x < nx; ++x) xn[x] = orc_dot(X + x * (int64_t)d, X + x * (int64_t)d, d);
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+    {
+        pair_t* tmp = (pair_t*)malloc(sizeof(pair_t) * (size_t)k);
+#pragma omp for schedule(dynamic, 16)
+        for (int64_t q = 0; q < nq; ++q) {
+            const float* qr = Q + q * (int64_t)d;
+            const float qn = orc_dot(qr, qr, d);
+            float* hs = out_s + q * (int64_t)k;  /* scores = -distance while selecting */
+            int64_t* hi = out_i + q * (int64_t)k;
+            for (int j = 0; j < k; ++j) { hs[j] = -FLT_MAX; hi[j] = -1; }
+            for (int64_t x = 0; x < nx; ++x) {
+                float dis = (qn + xn[x]) - 2.0f * orc_dot(qr, X + x * (int64_t)d, d);
+                if (dis < 0.0f) dis = 0.0f;
+                if (better(-dis, x, hs[0], hi[0])) {
+                    hs[0] = -dis; hi[0] = x;
+                    sift_down(hs, hi, k, 0);
+                }
+            }
+            for (int j = 0; j < k; ++j) { tmp[j].s = hs[j]; tmp[j].i = hi[j]; }
+            qsort(tmp, (size_t)k, sizeof(pair_t), cmp_pair);
+            for (int j = 0; j < k; ++j) {
+                const int ok = tmp[j].i >= 0;
+                hs[j] = ok ? -tmp[j].s : FLT_MAX;
+                hi[j] = ok ? tmp[j].i : -1;
+            }
+        }
+        free(tmp);
+    }
+    free(xn);
+    return 0;
+}
+
+/*
  * Merge n_lists candidate lists per query (layout [n_lists][nq][k_in]) into the
  * (score desc, id asc) top k_out. Entries with id -1 are ignored.
  */

@@ -1,0 +1,110 @@
+// IndexFlatL2 mode of the Flat index (FaissIndex with metric != "cosine",
+// src/serving/retrieval.py:96-100): exact squared-L2 k-nearest neighbours on
+// the same MFMA top-K kernels as the inner-product path.
+//
+// Ranking ‖q − x‖² ascending equals ranking q·x − ½‖x‖² descending, so both
+// sides are AUGMENTED once (rt_l2_augment_f32): item rows [x, −½‖x‖², 0, 0, 0],
+// query rows [q, 1, 0, 0, 0] (d + 4 columns, 16-byte rows), and
+// rt_flatip_topk selects on the augmented inner product. rt_l2_finish_f32 then
+// recomputes the reported distance of every selected item exactly as Faiss's
+// BLAS path defines it (exhaustive_L2sqr_blas: ‖q‖² + ‖x‖² − 2·q·x, clamped at
+// 0; norms and the dot as sequential fmaf chains, the order oracle/flatip.c
+// uses) and re-sorts each list by (distance asc, id asc) — Faiss's max-heap
+// keeps the lower id on exact ties. Unfilled slots: (FLT_MAX, −1).
+#include <float.h>
+
+#include "rt_common.h"
+#include "rt_sort.h"
+
+namespace rt {
+namespace l2 {
+
+// one wave per row: copy the d columns, the augmented column and the zero pad
+__global__ __launch_bounds__(256) void augment_kernel(const float* __restrict__ x, int64_t n, int d,
+                                                      float* __restrict__ out, int ld_out, int role) {
+    const int64_t r = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= n) return;
+    const float* xr = x + r * d;
+    float* o = out + r * ld_out;
+    float ss = 0.f;
+    for (int c = lane; c < d; c += 64) {
+        const float v = xr[c];
+        o[c] = v;
+        ss = __builtin_fmaf(v, v, ss);
+    }
+    ss = wave_sum(ss);
+    for (int c = d + lane; c < ld_out; c += 64) o[c] = (c == d) ? (role == 0 ? 1.f : -0.5f * ss) : 0.f;
+}
+
+__device__ __forceinline__ float seq_dot(const float* __restrict__ a, const float* __restrict__ b, int d) {
+    float acc = 0.f;
+    for (int j = 0; j < d; ++j) acc = __builtin_fmaf(a[j], b[j], acc);
+    return acc;
+}
+
+constexpr int kFinishN = 512;  // entries per wave (k <= 512)
+
+// one wave per query: exact distances of the k selected items, re-sorted
+__global__ __launch_bounds__(256) void finish_kernel(const float* __restrict__ q_aug, int ld_q,
+                                                     const float* __restrict__ x_aug, int ld_x, int d, int64_t nq,
+                                                     int k, float* __restrict__ scores, int64_t* __restrict__ ids,
+                                                     int64_t id_offset) {
+    __shared__ Cand buf[4][kFinishN];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + w;
+    if (q >= nq) return;  // wave-uniform; only wave-level LDS sync below
+    const float* qr = q_aug + q * ld_q;
+    const float qn = seq_dot(qr, qr, d);
+    const int n = next_pow2(k < 2 ? 2 : k);
+    Cand* b = buf[w];
+    for (int e = lane; e < n; e += 64) {
+        Cand c{-INFINITY, kEmptyId};
+        if (e < k) {
+            const int64_t id = ids[q * k + e];
+            if (id >= 0) {
+                const int64_t pos = id - id_offset;
+                const float* xr = x_aug + pos * ld_x;
+                const float xn = seq_dot(xr, xr, d);
+                const float ip = seq_dot(qr, xr, d);
+                float dis = (qn + xn) - 2.f * ip;
+                dis = dis < 0.f ? 0.f : dis;
+                c = Cand{-dis, static_cast<uint32_t>(pos)};
+            }
+        }
+        b[e] = c;
+    }
+    wave_lds_sync();
+    wave_sort_lds(b, n);
+    for (int e = lane; e < k; e += 64) {
+        const Cand c = b[e];
+        const bool ok = c.i != kEmptyId;
+        scores[q * k + e] = ok ? -c.s : FLT_MAX;
+        ids[q * k + e] = ok ? static_cast<int64_t>(c.i) + id_offset : -1;
+    }
+}
+
+}  // namespace l2
+}  // namespace rt
+
+using namespace rt;
+
+extern "C" int rt_l2_augment_f32(const float* x, int64_t n, int d, float* out, int ld_out, int role, void* stream) {
+    if (n < 0 || d <= 0 || ld_out < d + 1 || (role != 0 && role != 1)) return RT_ERR_INVALID;
+    if (n == 0) return RT_OK;
+    if (!x || !out) return RT_ERR_INVALID;
+    hipLaunchKernelGGL(l2::augment_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0,
+                       as_stream(stream), x, n, d, out, ld_out, role);
+    return check_launch("l2_augment_kernel");
+}
+
+extern "C" int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq, int k,
+                                float* scores, int64_t* ids, int64_t id_offset, void* stream) {
+    if (nq < 0 || d <= 0 || k <= 0 || ld_q < d || ld_x < d || id_offset < 0) return RT_ERR_INVALID;
+    if (k > l2::kFinishN) return RT_ERR_UNSUPPORTED;
+    if (nq == 0) return RT_OK;
+    if (!q_aug || !x_aug || !scores || !ids) return RT_ERR_INVALID;
+    hipLaunchKernelGGL(l2::finish_kernel, dim3(static_cast<unsigned>((nq + 3) / 4)), dim3(256), 0, as_stream(stream),
+                       q_aug, ld_q, x_aug, ld_x, d, nq, k, scores, ids, id_offset);
+    return check_launch("l2_finish_kernel");
+}

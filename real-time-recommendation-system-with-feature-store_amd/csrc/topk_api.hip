@@ -120,7 +120,7 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     if (!queries || !out_scores || !out_ids || (nx > 0 && !items)) return RT_ERR_INVALID;
     if (k > topk::kMaxK) return RT_ERR_UNSUPPORTED;
     if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return RT_ERR_INVALID;
-    if (dtype == RT_F32 ? (d % 4 != 0 || d > 128) : (d % 8 != 0 || d > 256)) return RT_ERR_UNSUPPORTED;
+    if (dtype == RT_F32 ? (d % 4 != 0 || d > 256) : (d % 8 != 0 || d > 256)) return RT_ERR_UNSUPPORTED;
     if (nx >= 0xFFFFFFFFll || (id_offset + nx) >= 0xFFFFFFFFll || id_offset < 0) return RT_ERR_UNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(queries) | reinterpret_cast<uintptr_t>(items)) & 15) return RT_ERR_INVALID;
     if (exclude_bits && exclude_words < (nx + 31) / 32) return RT_ERR_INVALID;

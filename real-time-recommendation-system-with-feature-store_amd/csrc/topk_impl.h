@@ -314,6 +314,11 @@ inline int list_k(bool f32, int k) {
     return k <= v2::kMaxKv2 ? -2 : 0;
 }
 
+// the v2 kernel's LDS image of an fp32 stage exceeds 160 KiB at d > 128: fp32
+// d in (128, 256] with k > 32 runs on v1
+template <typename T, int S>
+constexpr bool v2_fits() { return !(sizeof(T) == 4 && S > 64); }
+
 template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
     constexpr bool F32 = sizeof(T) == 4;
@@ -324,7 +329,9 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
             default: break;
         }
     }
-    if (list_k(F32, a.k) == -2) return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+    if constexpr (v2_fits<T, S>()) {
+        if (list_k(F32, a.k) == -2) return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+    }
     return v1::launch_S<T, S>(a, p.cap, p.splits, p.items_per_split, st);
 }
 
@@ -338,7 +345,9 @@ Shape shape_S(int k) {
     switch (list_k(sizeof(T) == 4, k)) {
         case 16: return {Cfg<T, S, 16>::QT, Cfg<T, S, 16>::NT, 0, 0};
         case 32: return {Cfg<T, S, 32>::QT, Cfg<T, S, 32>::NT, 0, 0};
-        case -2: return {v2::kQT, v2::kNT, v2::kCap, 2};
+        case -2:
+            if (v2_fits<T, S>()) return {v2::kQT, v2::kNT, v2::kCap, 2};
+            return {v1::kQT, v1::kNT, v1::cap_for(k), 1};
         default: return {v1::kQT, v1::kNT, v1::cap_for(k), 1};
     }
 }

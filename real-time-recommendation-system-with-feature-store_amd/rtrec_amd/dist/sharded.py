@@ -202,6 +202,9 @@ class ShardedFlatIPIndex:
         self.world, self.rank = _world(group)
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.storage_dtype = storage_dtype
+        if metric not in ("cosine", "inner_product"):
+            raise NotImplementedError("ShardedFlatIPIndex serves the inner-product metrics ('cosine', "
+                                      "'inner_product'); the L2 mode is single-GPU (HipFlatIPIndex)")
         self.metric = metric
         self.shard: Optional[torch.Tensor] = None
         self.begin = 0

@@ -125,6 +125,31 @@ def flatip_topk(queries: torch.Tensor, items: torch.Tensor, k: int,
     return scores, ids
 
 
+def l2_augment(x: torch.Tensor, role: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[n, d] fp32 → [n, d+4] augmented rows for the L2 mode (rt_l2_augment_f32):
+    role 0 (queries) appends 1, role 1 (items) appends -||x||^2/2."""
+    native.require_device(x, what="l2_augment")
+    if x.dtype != torch.float32 or x.dim() != 2:
+        raise ValueError("l2_augment expects fp32 [n, d]")
+    x = x.contiguous()
+    n, d = x.shape
+    if out is None:
+        out = torch.empty((n, d + 4), dtype=torch.float32, device=x.device)
+    call("rt_l2_augment_f32", ptr(x), n, d, ptr(out), out.shape[1], role, stream_of(x))
+    return out
+
+
+def flatl2_topk(q_aug: torch.Tensor, x_aug: torch.Tensor, d: int, k: int,
+                exclude_bits: Optional[torch.Tensor] = None, id_offset: int = 0
+                ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact squared-L2 k-NN on augmented rows (IndexFlatL2.search): (distances
+    [nq, k] ascending, ids [nq, k]); unfilled slots (FLT_MAX, -1)."""
+    s, i = flatip_topk(q_aug, x_aug, k, exclude_bits=exclude_bits, id_offset=id_offset)
+    call("rt_l2_finish_f32", ptr(q_aug), q_aug.shape[1], ptr(x_aug), x_aug.shape[1], d, q_aug.shape[0], k, ptr(s),
+         ptr(i), id_offset, stream_of(q_aug))
+    return s, i
+
+
 def topk_merge(scores: torch.Tensor, ids: torch.Tensor, k_out: int
                ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Merge candidate lists [n_lists, nq, k_in] into the (score desc, id asc) top k_out."""

@@ -74,6 +74,10 @@ class IndexBase(ABC):
 _STORAGE = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torch.bfloat16}
 
 
+MAX_DIM = 256   # rt_flatip_topk: d <= 256 (f32 d % 4 == 0, f16/bf16 d % 8 == 0)
+MAX_K = 512     # rt_flatip_topk / rt_topk_merge: k <= 512
+
+
 def _default_device() -> torch.device:
     if not torch.cuda.is_available():
         raise RuntimeError("HipFlatIPIndex needs a ROCm device (no CPU fallback in the MI355X build)")
@@ -84,7 +88,10 @@ class HipFlatIPIndex(IndexBase):
     """Exact inner-product index resident in HBM (FaissIndex ``Flat`` semantics).
 
     Config keys (retrieval.py:58-63): ``dimension`` (128), ``metric``
-    ("cosine" → normalize_L2 on build/add/search, else raw inner product),
+    ("cosine" → normalize_L2 on build/add/search + inner product, like
+    IndexFlatIP; any other value → squared L2 distances ascending, like
+    IndexFlatL2, float32 rows; "inner_product" → raw inner product, this
+    build's extension),
     ``index_factory`` (only recorded: every factory is served exactly),
     ``nprobe`` (ignored, exact), plus ``device`` and ``storage_dtype``
     ("float32" default = Faiss numerics; "float16"/"bfloat16" halve the bytes).
@@ -97,6 +104,18 @@ class HipFlatIPIndex(IndexBase):
         self.metric = self.config.get("metric", "cosine")
         self.nprobe = self.config.get("nprobe", 20)
         self.storage_dtype = _STORAGE[self.config.get("storage_dtype", "float32")]
+        # retrieval.py:96-100: "cosine" → IndexFlatIP on normalised rows, any other
+        # metric → IndexFlatL2; "inner_product" (this build's extension) → raw IP
+        self._l2 = self.metric not in ("cosine", "inner_product")
+        if self._l2 and self.storage_dtype != torch.float32:
+            raise ValueError("the L2 metric (IndexFlatL2) stores float32 rows, like Faiss")
+        # what rt_flatip_topk serves (include/rtrec_hip.h): fail at construction,
+        # not at the first search
+        d_max = MAX_DIM - 4 if self._l2 else MAX_DIM
+        step = 4 if self.storage_dtype == torch.float32 else 8
+        if not (0 < self.dimension <= d_max) or self.dimension % step:
+            raise ValueError(f"dimension {self.dimension} unsupported: the MI355X index serves d % {step} == 0, "
+                             f"d <= {d_max} for {self.metric!r} / {self.config.get('storage_dtype', 'float32')}")
         dev = self.config.get("device")
         self.device = torch.device(dev) if dev is not None else None
         self.index: Optional[torch.Tensor] = None   # [capacity, d] device rows; first current_size valid
@@ -127,16 +146,24 @@ class HipFlatIPIndex(IndexBase):
             kernels.l2_renorm_(t)
         return t
 
+    def _row_width(self) -> int:
+        """Stored row width: d, or d + 4 augmented columns in the L2 mode
+        ([x, -||x||^2/2, 0, 0, 0], rt_l2_augment_f32)."""
+        return self.dimension + 4 if self._l2 else self.dimension
+
     def _store(self, rows: torch.Tensor):
         rows = rows.to(self.storage_dtype)
         n_new = self.current_size + rows.shape[0]
         if self.index is None or self.index.shape[0] < n_new:
             cap = max(n_new, 2 * (self.index.shape[0] if self.index is not None else 0), 1024)
-            buf = torch.empty((cap, self.dimension), dtype=self.storage_dtype, device=self._dev())
+            buf = torch.empty((cap, self._row_width()), dtype=self.storage_dtype, device=self._dev())
             if self.index is not None and self.current_size:
                 buf[: self.current_size].copy_(self.index[: self.current_size])
             self.index = buf
-        self.index[self.current_size:n_new].copy_(rows)
+        if self._l2:
+            kernels.l2_augment(rows, 1, out=self.index[self.current_size:n_new])
+        else:
+            self.index[self.current_size:n_new].copy_(rows)
 
     # -- IndexBase ---------------------------------------------------------
     def build(self, embeddings: Array, ids: List[str]):
@@ -156,10 +183,17 @@ class HipFlatIPIndex(IndexBase):
 
     def search_tensors(self, query_embeddings: Array, k: int,
                        exclude_bits: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Device-level search: (scores [nq,k], positions [nq,k]) with -1 padding."""
+        """Device-level search: (scores [nq,k], positions [nq,k]) with -1 padding;
+        scores are inner products (descending) or, in the L2 mode, squared L2
+        distances (ascending, IndexFlatL2.search)."""
         if self.index is None:
             raise ValueError("Index not built yet")
+        if k > MAX_K:
+            raise ValueError(f"k={k} > {MAX_K}: the MI355X top-K kernels return at most {MAX_K} results per query")
         q = self._prepare(query_embeddings).to(self.storage_dtype)
+        if self._l2:
+            return kernels.flatl2_topk(kernels.l2_augment(q, 0), self.index[: self.current_size], self.dimension, k,
+                                       exclude_bits=exclude_bits)
         return kernels.flatip_topk(q, self.index[: self.current_size], k, exclude_bits=exclude_bits)
 
     def search(self, query_embeddings: Array, k: int = 10,
@@ -216,7 +250,7 @@ class HipFlatIPIndex(IndexBase):
     def vectors(self) -> np.ndarray:
         if self.index is None:
             return np.zeros((0, self.dimension), np.float32)
-        return self.index[: self.current_size].float().cpu().numpy()
+        return self.index[: self.current_size, : self.dimension].float().cpu().numpy()
 
     def save(self, path: str):
         """retrieval.py:248-273: ``<path>.faiss`` (IndexFlatIP/IndexFlatL2 binary
@@ -225,7 +259,7 @@ class HipFlatIPIndex(IndexBase):
             raise ValueError("No index to save")
         path = Path(path)
         path.parent.mkdir(parents=True, exist_ok=True)
-        write_flat_index(path.with_suffix(".faiss"), self.vectors(), self.metric == "cosine" or self.metric == "ip")
+        write_flat_index(path.with_suffix(".faiss"), self.vectors(), not self._l2)
         with open(path.with_suffix(".pkl"), "wb") as f:
             pickle.dump({"id_map": self.id_map, "reverse_id_map": self.reverse_id_map,
                          "current_size": self.current_size, "config": self.config}, f)
@@ -240,6 +274,8 @@ class HipFlatIPIndex(IndexBase):
         self.id_map = data["id_map"]
         self.reverse_id_map = data["reverse_id_map"]
         self.config = data.get("config", self.config)
+        self.metric = self.config.get("metric", self.metric)
+        self._l2 = self.metric not in ("cosine", "inner_product")
         self.dimension = vecs.shape[1]
         self.index = None
         self.current_size = 0

@@ -246,3 +246,75 @@ def test_index_save_load_roundtrip(K, tmp_path):
     idx2.load(str(tmp_path / "idx"))
     assert idx2.current_size == 300
     assert idx2.search(q, 20) == before
+
+
+# ---------------------------------------------------------------- fp32 d in (128, 256]
+@pytest.mark.parametrize("nq,nx,d,k", [(300, 3000, 256, 10), (200, 2500, 256, 32), (130, 2000, 256, 100),
+                                       (64, 1500, 192, 300), (33, 700, 160, 7)])
+def test_flatip_fp32_wide_rows_bit_exact(K, nq, nx, d, k):
+    """emb-256 fp32 corpora (FaissIndex has no dimension cap): register-list
+    kernel for k <= 32, candidate-buffer kernel above; bit-exact vs the oracle."""
+    rng = np.random.default_rng(nq + nx + d)
+    q = rng.standard_normal((nq, d)).astype(np.float32)
+    x = rng.standard_normal((nx, d)).astype(np.float32)
+    rs, ri = orc.flat_ip_search(q, x, k, nthreads=8)
+    gs, gi = K.flatip_topk(torch.from_numpy(q).cuda(), torch.from_numpy(x).cuda(), k)
+    assert np.array_equal(gi.cpu().numpy(), ri)
+    assert np.array_equal(gs.cpu().numpy(), rs)
+
+
+# ---------------------------------------------------------------- IndexFlatL2 mode
+def _l2_check(ref_s, ref_i, got_s, got_i):
+    """ids equal except inside near-tie groups; every returned (id, distance)
+    pair is the oracle's exact distance for that id (rt_l2_finish recomputes
+    it in the oracle's order)."""
+    for r in range(ref_i.shape[0]):
+        if not np.array_equal(ref_i[r], got_i[r]):
+            np.testing.assert_allclose(got_s[r], ref_s[r], rtol=1e-5, atol=1e-5)
+            kth = ref_s[r, -1]
+            assert set(ref_i[r][ref_s[r] < kth - 1e-4].tolist()) == set(got_i[r][got_s[r] < kth - 1e-4].tolist())
+        else:
+            assert np.array_equal(ref_s[r], got_s[r]), r
+
+
+@pytest.mark.parametrize("d,k,nx", [(128, 10, 3000), (128, 100, 3000), (64, 50, 70), (252, 20, 1000),
+                                    (32, 10, 6)])
+def test_flat_l2_index_vs_oracle(K, d, k, nx):
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex
+    rng = np.random.default_rng(d * 1000 + k)
+    emb = rng.standard_normal((nx, d)).astype(np.float32)
+    q = rng.standard_normal((64, d)).astype(np.float32)
+    q[:3] = emb[:3]                     # exact self-matches: distance 0 (clamped)
+    idx = HipFlatIPIndex({"dimension": d, "metric": "l2"})
+    idx.build(emb, [f"i{j}" for j in range(nx)])
+    gs, gi = idx.search_tensors(q, k)
+    rs, ri = orc.flat_l2_search(q, emb, k, nthreads=8)
+    _l2_check(rs, ri, gs.cpu().numpy(), gi.cpu().numpy())
+    assert gi[0, 0].item() == 0 and gs[0, 0].item() == 0.0
+    ids, dist = idx.search(q[:2], k)
+    assert ids[0][0] == "i0" and dist[0] == sorted(dist[0])
+
+
+def test_flat_l2_save_load_and_errors(K, tmp_path):
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex, read_flat_index
+    rng = np.random.default_rng(9)
+    emb = rng.standard_normal((500, 64)).astype(np.float32)
+    idx = HipFlatIPIndex({"dimension": 64, "metric": "euclidean"})
+    idx.build(emb[:400], [str(i) for i in range(400)])
+    idx.add(emb[400:], [str(i) for i in range(400, 500)])
+    q = rng.standard_normal((5, 64)).astype(np.float32)
+    before = idx.search(q, 30)
+    idx.save(str(tmp_path / "l2idx"))
+    vecs, is_ip = read_flat_index(tmp_path / "l2idx.faiss")
+    assert not is_ip and np.array_equal(vecs, emb)   # IxF2 layout, raw rows
+    idx2 = HipFlatIPIndex({"dimension": 64})
+    idx2.load(str(tmp_path / "l2idx"))
+    assert idx2.search(q, 30) == before
+    with pytest.raises(ValueError, match="dimension"):
+        HipFlatIPIndex({"dimension": 256, "metric": "l2"})
+    with pytest.raises(ValueError, match="dimension"):
+        HipFlatIPIndex({"dimension": 384})
+    with pytest.raises(ValueError, match="float32"):
+        HipFlatIPIndex({"dimension": 64, "metric": "l2", "storage_dtype": "float16"})
+    with pytest.raises(ValueError, match="k="):
+        idx.search(q, 513)
