@@ -85,13 +85,17 @@ def c2_setup(dev, rank, n_batches, dropout=0.2):
     return model, tables, batches, (uf, mf, bu, bp, bn)
 
 
+def _host_cores() -> int:
+    return len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(host, budget_s=10.0):
     """The oracle's torch-CPU restatement of the reference step (same math as
     src/training/trainers/two_tower.py:98-146) on a bounded sample of C2 batches."""
     from oracle import two_tower as orc
     from rtrec_amd.training.utils import create_two_tower_model_for_training
     uf, mf, bu, bp, bn = host
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = min(16, _host_cores())  # the box's CPU share for one GPU is 16 threads
     torch.set_num_threads(threads)
     torch.manual_seed(1234)
     model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
@@ -112,9 +116,66 @@ def cpu_baseline(host, budget_s=10.0):
         if el >= budget_s or steps >= 200:
             break
     pairs = steps * (1024 * 1024 + 1024 * 16)
-    return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "kind": "port",
+    return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "threads": threads,
+            "host_cores": _host_cores(), "kind": "port",
             "sample": f"{steps} C2 train steps (B=1024, N=16, emb 128) of oracle/two_tower.train_step on "
-                      f"torch-CPU, {el:.1f}s", "ms_per_step": 1000.0 * el / steps}
+                      f"torch-CPU with {threads} threads, {el:.1f}s", "ms_per_step": 1000.0 * el / steps}
+
+
+def _cpu_topk(q, x, k, qblock=4096, xblock=65536):
+    """Faiss-1.7.4-style exact IP top-k on the CPU (IndexFlatIP.search for
+    nq >= 20: blocked sgemm + per-row selection): blocked torch.mm + torch.topk,
+    fp32 (Faiss is fp32-only)."""
+    out_s, out_i = [], []
+    for q0 in range(0, q.shape[0], qblock):
+        qb = q[q0:q0 + qblock]
+        bs = bi = None
+        for x0 in range(0, x.shape[0], xblock):
+            sc = qb @ x[x0:x0 + xblock].T
+            ts, ti = torch.topk(sc, min(k, sc.shape[1]), dim=1)
+            ti += x0
+            if bs is None:
+                bs, bi = ts, ti
+            else:
+                cs, ci = torch.cat([bs, ts], 1), torch.cat([bi, ti], 1)
+                bs, j = torch.topk(cs, k, dim=1)
+                bi = torch.gather(ci, 1, j)
+        out_s.append(bs)
+        out_i.append(bi)
+    return torch.cat(out_s), torch.cat(out_i)
+
+
+def cpu_topk_baseline(budget_s=8.0):
+    """The top-K half of the metric on the host: C3 at full size (6,040 x 3,416
+    x 128, k=10) and C4 on a query sample (2,048 of the queries against the full
+    1M-item corpus, k=100, fp32), QPS extrapolated from the sample."""
+    threads = min(16, _host_cores())
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(7)
+    out = {}
+    q = torch.nn.functional.normalize(torch.randn(6040, 128, generator=g), dim=1)
+    x = torch.nn.functional.normalize(torch.randn(3416, 128, generator=g), dim=1)
+    _cpu_topk(q, x, 10)
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or (time.perf_counter() - t0 < budget_s / 4 and reps < 50):
+        _cpu_topk(q, x, 10)
+        reps += 1
+    el = (time.perf_counter() - t0) / reps
+    out["topk_c3"] = {"qps": 6040 / el, "ms": el * 1e3, "threads": threads, "host_cores": _host_cores(),
+                      "kind": "port", "sample": f"full C3 (6040x3416x128 fp32, k=10), {reps} reps: blocked "
+                                                "torch.mm + torch.topk (Faiss IndexFlatIP sgemm path)"}
+    x = torch.nn.functional.normalize(torch.randn(1_000_000, 128, generator=g), dim=1)
+    q = torch.nn.functional.normalize(torch.randn(2048, 128, generator=g), dim=1)
+    _cpu_topk(q[:256], x, 100)
+    t0 = time.perf_counter()
+    _cpu_topk(q, x, 100)
+    el = time.perf_counter() - t0
+    out["topk_c4"] = {"qps": 2048 / el, "ms_per_2048_queries": el * 1e3, "threads": threads,
+                      "host_cores": _host_cores(), "kind": "port",
+                      "sample": "2,048 queries x 1M-item corpus x 128 fp32, k=100 (C4 corpus; QPS extrapolated "
+                                "from the sample; Faiss is fp32-only, the GPU leg runs f16)"}
+    del x, q
+    return out
 
 
 def topk_extras(dev):
@@ -195,6 +256,88 @@ def topk_extras(dev):
     del u, p
     torch.cuda.empty_cache()
     return out
+
+
+def c2_with_feeder(dev, steps=30):
+    """The C2 step with the batch source inside the timed region: DeviceFeeder
+    (device shuffle + rt_sample_negatives over the train-interaction CSR, fused
+    gather ids) feeding eager FusedTrainStep calls — the reference spends
+    ≈345 ms per 1024-sample batch in its DataLoader here."""
+    from rtrec_amd.data.movielens import synthetic_movielens
+    from rtrec_amd.training.datasets.movielens import DeviceFeeder
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
+    data = synthetic_movielens(seed=0)
+    feeder = DeviceFeeder(data.train_interactions, data.users, data.movies, num_negatives=16, batch_size=1024,
+                          device=dev, seed=3)
+    torch.manual_seed(1234)
+    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 128, "hidden_layers": [256, 128],
+                                                        "dropout_rate": 0.2, "temperature": 0.05}).to(dev)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, max_norm=1.0)
+    it = iter(feeder)
+
+    def one():
+        b = next(it)
+        return step(b["user_table"], b["item_table"], b["item_table"], user_ids=b["user_ids"], pos_ids=b["pos_ids"],
+                    neg_ids=b["neg_ids"])
+    for _ in range(5):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    return {"ms_per_step": el * 1e3, "pairs_per_s": (1024 * 1024 + 1024 * 16) / el, "steps": steps,
+            "note": "eager steps, batch sampling (shuffle + on-device negatives) inside the timed region"}
+
+
+def c1_epoch(dev):
+    """Config C1 (BASELINE.json configs[0]): one epoch of rtrec_amd.train_movielens
+    at emb 64, batch 256, 16 negatives on the ML-1M-shaped stream (every train
+    batch; feeder, fused steps, validation, checkpoint)."""
+    import tempfile
+    from rtrec_amd import train_movielens as tm
+    with tempfile.TemporaryDirectory() as td:
+        args = tm.build_parser().parse_args(["--synthetic", "--epochs", "1", "--batch-size", "256",
+                                             "--embedding-dim", "64", "--checkpoint-dir", td + "/ckpt",
+                                             "--output-dir", td + "/out", "--init-seed", "1234"])
+        res = tm.run(args)
+    n = res["batches_last_epoch"]
+    return {"train_s": res["train_s"], "batches": n, "ms_per_batch": 1e3 * res["train_s"] / max(1, n),
+            "pairs_per_s": n * (256 * 256 + 256 * 16) / res["train_s"], "train_loss": res["train_losses"][0],
+            "val_loss": res["val_losses"][0],
+            "note": "one full epoch incl. validation and checkpoint writes (reference CPU: ~33 ms/step at this "
+                    "shape on the survey host, BASELINE.md §2)"}
+
+
+def _kernel_sources_sha() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(PKG, "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(csrc, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of ``kernel`` from the newest profiles/*_traffic.json
+    whose kernel-source hash matches the sources being run (rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes, tools/traffic_json.py); None if the PMC
+    profile is older than the kernels."""
+    import glob
+    sha = _kernel_sources_sha()
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
+        with open(path) as f:
+            tj = json.load(f)
+        if tj.get("kernel_sources_sha") != sha:
+            continue
+        tb = tj.get("bytes_per_launch", {}).get(kernel)
+        if tb is not None:
+            return float(tb), f"{os.path.relpath(path, REPO)}: " + tj.get("correction", "")
+    return None, f"no PMC profile of these kernel sources (sha {sha}) under profiles/"
 
 
 def topk_c4_scaling(dev, dist, rank, world, reps=3):
@@ -344,16 +487,11 @@ def main():
         roof = {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": achieved / PEAK_HBM_GBS, "traffic": None}
     # HBM traffic per launch of the dominant kernel: rocprofv3 FETCH_SIZE / WRITE_SIZE
-    # passes of this same bench command (profiles/r01_traffic.json, tools/traffic_json.py)
-    tpath = os.path.join(REPO, "profiles", "r01_traffic.json")
-    if os.path.exists(tpath):
-        with open(tpath) as f:
-            tj = json.load(f)
-        tb = tj.get("bytes_per_launch", {}).get(dominant)
-        if tb is not None:
-            roof["traffic"] = float(tb)
-            roof["traffic_unit"] = "bytes/launch (PMC)"
-            roof["traffic_source"] = "profiles/r01_traffic.json: " + tj.get("correction", "")
+    # passes of this same bench command over the SAME kernel sources (else null)
+    tb, tsrc = pmc_traffic(dominant)
+    roof["traffic"] = tb
+    roof["traffic_unit"] = "bytes/launch (PMC)"
+    roof["traffic_source"] = tsrc
     roof.update({"kernel": dominant, "launches_per_step": d["count"] / args.steps,
                  "measured": ("HIP events around each launch over an eager replay of the timed steps"
                               if args.graph else "HIP events around each launch inside the timed region"),
@@ -385,10 +523,25 @@ def main():
                 result["extras"] = topk_extras(dev)
             except Exception as e:  # extras never hide the headline
                 result["extras"] = {"error": repr(e)}
+            for name, fn in (("c2_with_feeder", lambda: c2_with_feeder(dev)), ("c1_train_epoch", lambda: c1_epoch(dev))):
+                try:
+                    result["extras"][name] = fn()
+                except Exception as e:
+                    result["extras"][name] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(host, args.cpu_budget)
+            try:
+                result["cpu_baseline"]["topk"] = cpu_topk_baseline()
+                ex = result.get("extras", {})
+                if "topk_c3" in ex and "qps" in ex["topk_c3"]:
+                    ex["topk_c3"]["vs_cpu"] = ex["topk_c3"]["qps"] / result["cpu_baseline"]["topk"]["topk_c3"]["qps"]
+            except Exception as e:
+                result["cpu_baseline"]["topk"] = {"error": repr(e)}
     if scaling is not None:
         result.setdefault("extras", {})["topk_c4_1m_sharded"] = scaling
+        cb = result.get("cpu_baseline", {}).get("topk", {}).get("topk_c4")
+        if cb and "qps" in scaling:
+            scaling["vs_cpu"] = scaling["qps"] / cb["qps"]
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

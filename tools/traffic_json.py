@@ -5,10 +5,25 @@ bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B). FETCH_SIZE is doubled as
 MI355X_MICROARCH.md prescribes for gfx950 (it tallies 128-B requests at 64 B
 for wide 16-B-per-lane reads, the access width of these kernels).
 Usage: traffic_json.py c2_pmc.txt topk_pmc.txt > profiles/r01_traffic.json"""
+import hashlib
 import json
+import os
 import re
 import sys
 from collections import defaultdict
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    "real-time-recommendation-system-with-feature-store_amd", "csrc")
+
+
+def kernel_sources_sha() -> str:
+    """Same hash as bench.py::_kernel_sources_sha (which refuses a stale profile)."""
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(CSRC)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(CSRC, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 FAMILY = {"linear_fwd_kernel": ["linear_fwd"], "linear_bwd_dz_kernel": ["linear_bwd_dz"],
           "linear_bwd_dw_kernel": ["linear_bwd_dw"], "loss_fwd_kernel": ["loss_fwd_bwd"],
@@ -46,5 +61,6 @@ for (name, fam), b in tot.items():
 json.dump({"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes: "
                      "bench.py --steps 10 --warmup 3 --no-extras --no-cpu-baseline and tools/prof_topk.py 100 2",
            "correction": "bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halves wide 16-B/lane reads)",
+           "kernel_sources_sha": kernel_sources_sha(),
            "bytes_per_launch": {k: round(v) for k, v in per.items()}}, sys.stdout, indent=1)
 print()
