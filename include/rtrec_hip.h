@@ -237,6 +237,10 @@ typedef struct {
     float* dsrc;             /* [m, k] input grad (first layer), or NULL */
     int64_t seg_split;       /* as in rt_linear_fwd_args: g_stats, save_mean/invstd,
                                 prev_mean/invstd and g_prev_stats are then [2][...] */
+    double* dbias_slots;     /* optional fp64 [RT_STAT_SLOTS][n], caller-zeroed: the dz launch
+                                adds each row block's column sums of dz (slot = block % SLOTS)
+                                and the dW launch folds the slots into dbias — bounded
+                                same-address contention; NULL = the dW launch sums dz itself */
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);

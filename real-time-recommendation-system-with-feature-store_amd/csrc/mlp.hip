@@ -606,6 +606,18 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
             }
         }
     }
+    if (a.dbias && a.dbias_slots) {
+        // dbias partials: this block's column sums of dz into fp64 slot bid % SLOTS
+        // (the dW launch folds the slots; contention per address = blocks / SLOTS)
+        __syncthreads();
+        double* sl = a.dbias_slots + static_cast<int64_t>(bid % RT_STAT_SLOTS) * n;
+        for (int c = tid; c < n; c += 256) {
+            float cs = 0.f;
+#pragma unroll 8
+            for (int r = 0; r < FM; ++r) cs += Dz[r * ldz + c];
+            atomicAdd(&sl[c], static_cast<double>(cs));
+        }
+    }
     if (bid == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
         // dgamma/dbeta of each BN batch (segment), summed like two tower calls' grads
         for (int c = tid; c < n; c += 256) {
@@ -738,21 +750,26 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
 // backward 2: dW[n][k] += Σ_r dz[r][n] · A[r][k] (+ dbias[n] += Σ_r dz[r][n]),
 // M split over the blocks of a group
 // ---------------------------------------------------------------------------
-// Block = one 64(n) x 64(k) tile of dW over a contiguous row range, 4 waves
-// each owning a 32 x 32 quarter. Rows stream in chunks of 128: every thread
-// loads a float4 of dz and of A for 8 rows (global loads of chunk c+1 are in
-// flight while chunk c is multiplied), applies the A prologue (act → BN
-// affine → dropout, the forward's own transform) on registers and writes both
-// tiles TRANSPOSED into LDS ([col][row], 16-B aligned rows), so each lane's
-// MFMA operands are contiguous: lane half h reduces rows h·64 + s, and one
-// ds_read_b128 feeds 4 v_mfma_f32_32x32x2_f32 k-steps. The tile is added to
-// dW with one fp32 atomic per element per block (<= 128 splits, see the host).
+// Block = one BN(n) x BK(k) tile of dW over a contiguous row range, 8 waves in
+// two row groups of 4 (each group's waves own the tile's 32x32 sub-tiles; the
+// groups take alternate row pairs and are summed through LDS at the end).
+// Rows stream in 32-row chunks staged ROW-MAJOR in LDS (float4 loads → one
+// ds_write_b128, no transposition), double-buffered: chunk c+1's global loads
+// are in flight during chunk c's MFMAs and land in the other buffer. The MFMA
+// operands are read straight from the row-major tiles: for the row pair
+// (2p, 2p+1) lane c of half h reads dz[2p+h][n-col c] and A[2p+h][k-col c]
+// (ds_read_b32; row strides ≡ 32 mod 64 banks, so the halves never collide),
+// i.e. v_mfma_f32_32x32x2_f32 with the row pair as its k = 2. A goes through
+// the forward's own prologue (act → BN affine → dropout) while it is staged.
+// The tile is added to dW with one fp32 atomic per element per block (one
+// 128-B row segment per lane half); blocks of k-tile 0 also add dbias.
 //   PRO: 0 raw A, 1 piecewise-linear act, 2 same + dropout, 3 generic act.
-constexpr int DW_T = 64;          // n and k per block
-constexpr int DW_R = 128;         // rows per chunk
-constexpr int DW_P = DW_R / 16;   // rows per staging thread per chunk
-constexpr int DW_LD = DW_R + 4;   // LDS row stride (floats) of the transposed tiles
+constexpr int DW_R = 32;          // rows per chunk
+constexpr int DW_G = 2;           // row groups (waves 4g..4g+3)
+constexpr int DW_NT = 256 * DW_G; // threads per block
 constexpr int DW_MAXR = 2048;     // rows per split whose gather ids are staged in LDS
+
+__host__ __device__ constexpr int dw_ld(int x) { return x + ((x / 32) % 2 == 0 ? 32 : 0); }  // ≡ 32 mod 64
 
 template <int PRO>
 __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, int c, float sc, float sh, float v) {
@@ -770,41 +787,48 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
     }
 }
 
-template <int PRO>
-__global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
+template <int BN, int BK, int PRO, bool VEC>  // VEC: n, k, ld_src multiples of 4, 16-B aligned rows
+__global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
+    constexpr int NTN = BN / 32, WK = 4 / NTN, T = (BK / 32) / WK;
+    static_assert(NTN * 32 == BN && 4 % NTN == 0 && T >= 1 && T * WK * 32 == BK, "dW tile");
+    constexpr int LDN = dw_ld(BN), LDK = dw_ld(BK);
+    constexpr int VN = BN / 4, VK = BK / 4;  // float4 per row
+    constexpr int LN = (DW_R * VN + DW_NT - 1) / DW_NT, LK = (DW_R * VK + DW_NT - 1) / DW_NT;
+    static_assert(DW_NT % VN == 0 && DW_NT % VK == 0, "fixed staging columns per thread");
+    static_assert(2 * DW_R * LDN >= 4 * T * 16 * 64, "row-group reduction fits in the dz buffers");
+    static_assert(2 * DW_R * LDK >= (DW_NT / 64) * VN * 4, "dbias partials fit in the A buffers");
+    __shared__ __attribute__((aligned(16))) float Ld[2][DW_R * LDN];
+    __shared__ __attribute__((aligned(16))) float La[2][DW_R * LDK];
+    __shared__ int srow[DW_MAXR];
+
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args a = g1 ? L.a1 : L.a0;  // by value: fields loaded once
     const int64_t rows_per_split = g1 ? L.rps1 : L.rps0;
-    // flattened (n tile, k tile, split) of this block within its group
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
     const unsigned tn = g1 ? L.tn1 : L.tn0, tk = g1 ? L.tk1 : L.tk0;
     const unsigned bx = bid % tn, by = (bid / tn) % tk, bz = bid / (tn * tk);
-    const bool vec = g1 ? L.vec1 : L.vec0;  // n, k, ld_src multiples of 4, 16-B aligned rows
-    __shared__ __attribute__((aligned(16))) float dzT[DW_T][DW_LD];
-    __shared__ __attribute__((aligned(16))) float aT[DW_T][DW_LD];
-    __shared__ int srow[DW_MAXR];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int n0 = static_cast<int>(bx) * DW_T, k0 = static_cast<int>(by) * DW_T;
+    const int tid = threadIdx.x, lane = tid & 63, wg = tid >> 6, w = wg & 3, grp = wg >> 2, h = lane >> 5,
+              c = lane & 31;
+    const int n0 = static_cast<int>(bx) * BN, k0 = static_cast<int>(by) * BK;
     const int64_t r_begin = static_cast<int64_t>(bz) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
     if (r_begin >= m) return;  // a padding split (block-uniform, before any barrier)
     const bool gather = a.ids != nullptr;
     const bool two = a.seg_split > 0;
 
-    // staging role: 4 consecutive columns (c4) of rows rr + 16p, p = 0..3
-    const int c4 = tid >> 4, rr = tid & 15;
-    const int gn = n0 + 4 * c4, gk = k0 + 4 * c4;
+    // staging columns of this thread (the same for every staged row)
+    const int cn = (tid % VN) * 4, ck = (tid % VK) * 4;
+    const int gn = n0 + cn, gk = k0 + ck;
     // BN affine of the previous block for this thread's 4 A columns, per row segment
-    // (named float4s, not arrays: a per-row segment select must stay a v_cndmask)
     float4 sc0 = make_float4(1.f, 1.f, 1.f, 1.f), sc1 = sc0;
     float4 sh0 = make_float4(0.f, 0.f, 0.f, 0.f), sh1 = sh0;
     if (a.prev_mode == 1 || a.prev_mode == 2) {
         auto aff = [&](int sg, int i, float& scv, float& shv) {
-            const int c = gk + i;
+            const int cc = gk + i;
             const int so = two ? sg * k : 0;
-            if (c < k) bn_affine(a.prev_gamma[c], a.prev_beta[c], a.prev_mean[so + c], a.prev_invstd[so + c], scv, shv);
+            if (cc < k) bn_affine(a.prev_gamma[cc], a.prev_beta[cc], a.prev_mean[so + cc], a.prev_invstd[so + cc], scv, shv);
         };
         aff(0, 0, sc0.x, sh0.x); aff(0, 1, sc0.y, sh0.y); aff(0, 2, sc0.z, sh0.z); aff(0, 3, sc0.w, sh0.w);
         aff(1, 0, sc1.x, sh1.x); aff(1, 1, sc1.y, sh1.y); aff(1, 2, sc1.z, sh1.z); aff(1, 3, sc1.w, sh1.w);
@@ -813,103 +837,171 @@ __global__ __launch_bounds__(256) void linear_bwd_dw_kernel(BwdLaunch L) {
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
                   pseed, nullptr, nullptr};
     const float slope = act_slope(a.prev_act);
-    const bool do_bias = a.dbias != nullptr && by == 0;
+    // dbias: folded from the dz launch's fp64 slots by block 0, or (no slots)
+    // summed here by the k-tile-0 blocks
+    if (a.dbias && a.dbias_slots && bid == 0) {
+        for (int cc = tid; cc < n; cc += DW_NT) {
+            double v = 0.0;
+#pragma unroll
+            for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) v += a.dbias_slots[static_cast<int64_t>(sl) * n + cc];
+            atomicAdd(&a.dbias[cc], static_cast<float>(v));
+        }
+    }
+    const bool do_bias = a.dbias != nullptr && a.dbias_slots == nullptr && by == 0;
 
     if (gather) {
-        for (int64_t t = tid; t < r_end - r_begin; t += 256) {
+        for (int64_t t = tid; t < r_end - r_begin; t += DW_NT) {
             const int64_t id = a.ids[r_begin + t];
             srow[t] = (id < 0 || id >= a.src_rows) ? -1 : static_cast<int>(id);
         }
         __syncthreads();
     }
 
-    float4 dv[DW_P], av[DW_P];  // one chunk's staged values (prefetch registers)
-    float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-    f32x16 acc = f32x16{};
-    const float* ar = &dzT[(w & 1) * 32 + c32][h * (DW_R / 2)];
-    const float* br = &aT[(w >> 1) * 32 + c32][h * (DW_R / 2)];
-    auto load = [&](int64_t nx) {  // one chunk's dz / A float4s into registers
+    float4 rd[LN], ra[LK];  // one chunk's staged values (prefetch registers)
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](int64_t base) {
 #pragma unroll
-        for (int p = 0; p < DW_P; ++p) {
-            const int64_t r = nx + rr + 16 * p;
-            dv[p] = make_float4(0.f, 0.f, 0.f, 0.f);
-            av[p] = dv[p];
-            if (r >= r_end) continue;
-            const float* dz = a.dz_ws + r * n + gn;
-            const int64_t sr = gather ? srow[r - r_begin] : r;
-            const float* ap = a.src + sr * a.ld_src + gk;
-            if (vec) {
-                if (gn < n) dv[p] = *reinterpret_cast<const float4*>(dz);
-                if (gk < k && sr >= 0) av[p] = *reinterpret_cast<const float4*>(ap);
-            } else {
-                if (gn < n) dv[p].x = dz[0];
-                if (gn + 1 < n) dv[p].y = dz[1];
-                if (gn + 2 < n) dv[p].z = dz[2];
-                if (gn + 3 < n) dv[p].w = dz[3];
-                if (sr >= 0) {
-                    if (gk < k) av[p].x = ap[0];
-                    if (gk + 1 < k) av[p].y = ap[1];
-                    if (gk + 2 < k) av[p].z = ap[2];
-                    if (gk + 3 < k) av[p].w = ap[3];
+        for (int j = 0; j < LN; ++j) {
+            const int e = tid + DW_NT * j, row = e / VN;
+            const int64_t r = base + row;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < DW_R * VN && r < r_end) {
+                const float* dz = a.dz_ws + r * n + gn;
+                if constexpr (VEC) {
+                    if (gn < n) v = *reinterpret_cast<const float4*>(dz);
+                } else {
+                    if (gn < n) v.x = dz[0];
+                    if (gn + 1 < n) v.y = dz[1];
+                    if (gn + 2 < n) v.z = dz[2];
+                    if (gn + 3 < n) v.w = dz[3];
                 }
+            }
+            rd[j] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < LK; ++j) {
+            const int e = tid + DW_NT * j, row = e / VK;
+            const int64_t r = base + row;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e < DW_R * VK && r < r_end) {
+                const int64_t sr = gather ? srow[r - r_begin] : r;
+                if (sr >= 0) {
+                    const float* ap = a.src + sr * a.ld_src + gk;
+                    if constexpr (VEC) {
+                        if (gk < k) v = *reinterpret_cast<const float4*>(ap);
+                    } else {
+                        if (gk < k) v.x = ap[0];
+                        if (gk + 1 < k) v.y = ap[1];
+                        if (gk + 2 < k) v.z = ap[2];
+                        if (gk + 3 < k) v.w = ap[3];
+                    }
+                }
+            }
+            ra[j] = v;
+        }
+    };
+    auto store = [&](int buf, int64_t base) {
+#pragma unroll
+        for (int j = 0; j < LN; ++j) {
+            const int e = tid + DW_NT * j, row = e / VN;
+            if (e < DW_R * VN) {
+                *reinterpret_cast<float4*>(&Ld[buf][row * LDN + cn]) = rd[j];
+                bsum.x += rd[j].x; bsum.y += rd[j].y; bsum.z += rd[j].z; bsum.w += rd[j].w;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < LK; ++j) {
+            const int e = tid + DW_NT * j, row = e / VK;
+            if (e < DW_R * VK) {
+                const int64_t r = base + row;
+                const bool ok = r < r_end && (!gather || srow[r - r_begin] >= 0);
+                const bool hi_seg = two && r >= a.seg_split;
+                const float4 scs = hi_seg ? sc1 : sc0, shs = hi_seg ? sh1 : sh0;
+                float4 v;
+                v.x = (ok && gk < k) ? pro_col<PRO>(pro, slope, r, gk, scs.x, shs.x, ra[j].x) : 0.f;
+                v.y = (ok && gk + 1 < k) ? pro_col<PRO>(pro, slope, r, gk + 1, scs.y, shs.y, ra[j].y) : 0.f;
+                v.z = (ok && gk + 2 < k) ? pro_col<PRO>(pro, slope, r, gk + 2, scs.z, shs.z, ra[j].z) : 0.f;
+                v.w = (ok && gk + 3 < k) ? pro_col<PRO>(pro, slope, r, gk + 3, scs.w, shs.w, ra[j].w) : 0.f;
+                *reinterpret_cast<float4*>(&La[buf][row * LDK + ck]) = v;
             }
         }
     };
-    if (r_begin < r_end) load(r_begin);
-    for (int64_t c0 = r_begin; c0 < r_end; c0 += DW_R) {
-        __syncthreads();  // the previous chunk's MFMA reads are done
-        // stage: dz as is, A through the prologue, both transposed into LDS
+
+    f32x16 acc[T];
 #pragma unroll
-        for (int p = 0; p < DW_P; ++p) {
-            const int row = rr + 16 * p;
-            const int64_t r = c0 + row;
-            const bool hi_seg = two && r >= a.seg_split;
-            const bool ok = r < r_end && (!gather || srow[r - r_begin] >= 0);
-            const float d4[4] = {dv[p].x, dv[p].y, dv[p].z, dv[p].w};
-            const float a4[4] = {av[p].x, av[p].y, av[p].z, av[p].w};
-            const float4 scs = hi_seg ? sc1 : sc0, shs = hi_seg ? sh1 : sh0;
-            const float scv[4] = {scs.x, scs.y, scs.z, scs.w}, shv[4] = {shs.x, shs.y, shs.z, shs.w};
+    for (int t = 0; t < T; ++t) acc[t] = f32x16{};
+    const int ncol = (w % NTN) * 32 + c;       // this lane's dz column inside the tile
+    const int kcol0 = (w / NTN) * T * 32 + c;  // this lane's first A column inside the tile
+    int buf = 0;
+    load(r_begin);
+    store(0, r_begin);
+    __syncthreads();
+    for (int64_t base = r_begin; base < r_end; base += DW_R) {
+        const bool more = base + DW_R < r_end;  // block-uniform
+        if (more) load(base + DW_R);            // in flight during the MFMAs below
+        // row pairs grp, grp + DW_G, ...: lane half h reads row 2·pair + h
+        const float* dl = &Ld[buf][(2 * grp + h) * LDN + ncol];
+        const float* al = &La[buf][(2 * grp + h) * LDK + kcol0];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                dzT[4 * c4 + i][row] = d4[i];
-                bsum[i] += d4[i];
-                aT[4 * c4 + i][row] =
-                    (ok && gk + i < k) ? pro_col<PRO>(pro, slope, r, gk + i, scv[i], shv[i], a4[i]) : 0.f;
-            }
+        for (int i = 0; i < DW_R / (2 * DW_G); ++i) {
+            const float av = dl[2 * DW_G * i * LDN];
+#pragma unroll
+            for (int t = 0; t < T; ++t) acc[t] = mfma(av, al[2 * DW_G * i * LDK + 32 * t], acc[t]);
         }
+        if (more) store(buf ^ 1, base + DW_R);
         __syncthreads();
-        // next chunk's loads fly during this chunk's MFMAs
-        if (c0 + DW_R < r_end) load(c0 + DW_R);
-#pragma unroll
-        for (int s = 0; s < DW_R / 2; s += 4) {
-            const float4 x = *reinterpret_cast<const float4*>(ar + s);
-            const float4 y = *reinterpret_cast<const float4*>(br + s);
-            acc = mfma(x.x, y.x, acc);
-            acc = mfma(x.y, y.y, acc);
-            acc = mfma(x.z, y.z, acc);
-            acc = mfma(x.w, y.w, acc);
-        }
+        buf ^= 1;
     }
 
-    // acc[r] = dW[n0 + 32(w&1) + (r&3) + 8(r>>2) + 4h][k0 + 32(w>>1) + c32]
-    const int ok_k = k0 + (w >> 1) * 32 + c32;
-    if (ok_k < k) {
+    // dbias: column sums of dz over this block's rows. Threads sharing the
+    // staging columns cn (lanes l ^ 16·j when VN = 16, l ^ 32 when VN = 32) are
+    // summed by shuffles, the 8 waves through LDS, then ONE atomic per column
+    // per block (same-address float atomics serialise: 8 per block measured
+    // 40-80 µs at the C2 shapes). Row group 1 hands its accumulators to group 0
+    // through the (idle) dz buffers, the dbias partials go through the A buffers.
+    float* red = &Ld[0][0];
+    float* bred = &La[0][0];  // [8 waves][VN][4]
+    if (do_bias) {
+#pragma unroll
+        for (int o = VN; o < 64; o <<= 1) {
+            bsum.x += __shfl_xor(bsum.x, o, 64);
+            bsum.y += __shfl_xor(bsum.y, o, 64);
+            bsum.z += __shfl_xor(bsum.z, o, 64);
+            bsum.w += __shfl_xor(bsum.w, o, 64);
+        }
+        if (lane < VN) *reinterpret_cast<float4*>(&bred[(wg * VN + lane) * 4]) = bsum;
+    }
+    if (grp == 1) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[((w * T + t) * 16 + r) * 64 + lane] = acc[t][r];
+    }
+    __syncthreads();
+    if (do_bias && tid < VN) {
+        float4 sb = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int o = 0; o < DW_NT / 64; ++o) {
+            const float4 v = *reinterpret_cast<const float4*>(&bred[(o * VN + tid) * 4]);
+            sb.x += v.x; sb.y += v.y; sb.z += v.z; sb.w += v.w;
+        }
+        const int cb = n0 + tid * 4;
+        if (cb < n) atomicAdd(&a.dbias[cb], sb.x);
+        if (cb + 1 < n) atomicAdd(&a.dbias[cb + 1], sb.y);
+        if (cb + 2 < n) atomicAdd(&a.dbias[cb + 2], sb.z);
+        if (cb + 3 < n) atomicAdd(&a.dbias[cb + 3], sb.w);
+    }
+    if (grp == 1) return;
+    // acc[t][r] = dW[n0 + ncol-tile + (r&3) + 8(r>>2) + 4h][k0 + kcol0 + 32t]
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int kk = k0 + kcol0 + 32 * t;
+        if (kk >= k) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int on = n0 + (w & 1) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (on < n) atomicAdd(&a.dw[static_cast<int64_t>(on) * k + ok_k], acc[r]);
-        }
-    }
-    if (do_bias) {  // the 16 threads of a column group are 16 consecutive lanes
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int o = 1; o < 16; o <<= 1) bsum[i] += __shfl_xor(bsum[i], o, 64);
-        }
-        if (rr == 0) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                if (gn + i < n) atomicAdd(&a.dbias[gn + i], bsum[i]);
+            const int nn = n0 + (w % NTN) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const float v = acc[t][r] + red[((w * T + t) * 16 + r) * 64 + lane];
+            if (nn < n) atomicAdd(&a.dw[static_cast<int64_t>(nn) * k + kk], v);
         }
     }
 }
@@ -1050,20 +1142,20 @@ extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream
     return rt_linear_bwd_dz_f32_multi(args, 1, stream);
 }
 
-// dW tiling of one Linear: ~1024 blocks (4 per CU), whole 128-row chunks, <= 64
-// splits per tile (atomics per dW element; 128 for <= 4 tiles), <= DW_MAXR
-// rows per split (gather ids staged in LDS)
-static void dw_plan(const rt_linear_bwd_args& a, unsigned& tn, unsigned& tk, int64_t& splits, int64_t& rps) {
-    tn = static_cast<unsigned>((a.n + mlp::DW_T - 1) / mlp::DW_T);
-    tk = static_cast<unsigned>((a.k + mlp::DW_T - 1) / mlp::DW_T);
-    splits = (1024 + tn * tk - 1) / (tn * tk);
+// dW tiling of one Linear: 64x64 tiles (128x32 when k <= 32), ~512 blocks
+// (2 per CU), whole 32-row chunks, <= 64 splits per tile (float atomics per dW
+// element), <= DW_MAXR rows per split (gather ids staged in LDS)
+static void dw_plan(const rt_linear_bwd_args& a, bool small_k, unsigned& tn, unsigned& tk, int64_t& splits,
+                    int64_t& rps) {
+    const int bn = small_k ? 128 : 64, bk = small_k ? 32 : 64;
+    tn = static_cast<unsigned>((a.n + bn - 1) / bn);
+    tk = static_cast<unsigned>((a.k + bk - 1) / bk);
+    const int64_t tiles = static_cast<int64_t>(tn) * tk;
+    splits = (512 + tiles - 1) / tiles;
+    const int64_t cap = 64;
+    if (splits > cap) splits = cap;
     const int64_t max_splits = (a.m + mlp::DW_R - 1) / mlp::DW_R;
     if (splits > max_splits) splits = max_splits;
-    // measured (C2 step A/B, lib/variants): a cap of 64 (→ 46 splits of 3 chunks
-    // at m = 17,408) beats 16/32 (slower by 7 % / 2 %) and 128/256 for 8 tiles
-    // (layer 2); 128 for 4 tiles (layers 1 and 3)
-    const int64_t cap = tn * tk <= 4 ? 128 : 64;
-    if (splits > cap) splits = cap;
     if (splits < 1) splits = 1;
     rps = (a.m + splits - 1) / splits;
     rps = (rps + mlp::DW_R - 1) / mlp::DW_R * mlp::DW_R;
@@ -1076,13 +1168,17 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     mlp::BwdLaunch L{};
     unsigned blocks[2] = {0u, 0u};
     int pro = -1;
+    bool small_k = true;
     for (int g = 0; g < n_args; ++g) {
         const int v = validate_bwd(&args[g]);
         if (v) return v;
+        small_k = small_k && args[g].k <= 32;
+    }
+    for (int g = 0; g < n_args; ++g) {
         const rt_linear_bwd_args& a = args[g];
         unsigned tn = 0, tk = 0;
         int64_t splits = 0, rps = 0;
-        if (a.m > 0) dw_plan(a, tn, tk, splits, rps);
+        if (a.m > 0) dw_plan(a, small_k, tn, tk, splits, rps);
         const int64_t nb = static_cast<int64_t>(tn) * tk * splits;
         if (nb > (1ll << 30)) return RT_ERR_UNSUPPORTED;
         blocks[g] = static_cast<unsigned>(nb);
@@ -1110,8 +1206,19 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     if (total == 0) return RT_OK;
     const dim3 grid(total);
     hipStream_t st = as_stream(stream);
-#define RT_DW(P) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<P>), grid, dim3(256), 0, st, L)
-    switch (pro) { case 0: RT_DW(0); break; case 1: RT_DW(1); break; case 2: RT_DW(2); break; default: RT_DW(3); }
+    const bool vec = L.vec0 && L.vec1;
+#define RT_DW(BN, BK, P)                                                                                          \
+    do {                                                                                                          \
+        if (vec) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, true>), grid, dim3(mlp::DW_NT), 0, st, L);  \
+        else hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, false>), grid, dim3(mlp::DW_NT), 0, st, L);     \
+    } while (0)
+    if (small_k) {
+        switch (pro) { case 0: RT_DW(128, 32, 0); break; case 1: RT_DW(128, 32, 1); break;
+                       case 2: RT_DW(128, 32, 2); break; default: RT_DW(128, 32, 3); }
+    } else {
+        switch (pro) { case 0: RT_DW(64, 64, 0); break; case 1: RT_DW(64, 64, 1); break;
+                       case 2: RT_DW(64, 64, 2); break; default: RT_DW(64, 64, 3); }
+    }
 #undef RT_DW
     return check_launch("linear_bwd_dw_kernel");
 }

@@ -204,8 +204,10 @@ STAT_SLOTS = 16  # RT_STAT_SLOTS (include/rtrec_hip.h): BN sums are [slots][2][w
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
-    """fp64 words of BN column sums one forward (or backward) of the chain needs."""
-    return max(1, n_seg * STAT_SLOTS * 2 * sum(b.linear.out_features for b in blocks[:-1]))
+    """fp64 words of BN column sums one forward (or backward) of the chain needs,
+    plus the dbias slots of every Linear ([STAT_SLOTS][n], backward)."""
+    return max(1, n_seg * STAT_SLOTS * 2 * sum(b.linear.out_features for b in blocks[:-1])
+               + STAT_SLOTS * sum(b.linear.out_features for b in blocks))
 
 
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
@@ -414,6 +416,10 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
     for wdt in widths:
         gstats.append(gst_arena[off:off + n_seg * STAT_SLOTS * 2 * wdt])
         off += n_seg * STAT_SLOTS * 2 * wdt
+    bslots = []  # dbias slots of Linear li (both BN segments add into the same slots)
+    for b in blocks:
+        bslots.append(gst_arena[off:off + STAT_SLOTS * b.linear.out_features])
+        off += STAT_SLOTS * b.linear.out_features
     gs: List[Optional[torch.Tensor]] = [None] * L
     dsrc = torch.empty((m, blocks[0].linear.in_features), dtype=torch.float32, device=dev) if want_dsrc else None
     keep = [dout, dz_ws, gst_arena]
@@ -425,6 +431,7 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         a.w = lin.weight.data_ptr()
         a.dw = slab.grad_of(lin.weight).data_ptr()
         a.dbias = slab.grad_of(lin.bias).data_ptr() if lin.bias is not None else None
+        a.dbias_slots = bslots[li].data_ptr() if lin.bias is not None else None
         a.dz_ws = dz_ws.data_ptr()
         a.seed_offset = seed_offset.data_ptr() if seed_offset is not None else None
         a.seg_split = ctx.seg_split

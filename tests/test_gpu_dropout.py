@@ -84,7 +84,8 @@ def test_dropout_mask_rate_scale_and_backward(device, bn_train):
     # kept values are scaled by 1/(1-p) (the identity Linear passes them through exactly)
     scale = 1.0 / (1.0 - P)
     want = a * scale
-    torch.testing.assert_close(out[keep], want[keep], rtol=2e-6 if not bn_train else 2e-5, atol=1e-6)
+    torch.testing.assert_close(out[keep], want[keep], rtol=2e-6 if not bn_train else 2e-5,
+                               atol=1e-6 if not bn_train else 1e-5)  # BN-train: batch stats of two fp32 reductions
 
     # backward through the same ctx: grads must use the forward's mask
     dout = torch.randn(M, H, device=device, generator=g)
