@@ -186,6 +186,10 @@ typedef struct {
                                 below (prev_stats, save_mean/invstd, stats_out) is then
                                 [2][...] (segment-major), running stats are updated segment 0
                                 then segment 1, num_batches_tracked += 2. */
+    double* zero_buf;        /* optional fp64 [zero_words] set to 0 by the launch before any
+                                other work (a step's first launch clears the next
+                                accumulators: loss triple, per-tensor grad norms) */
+    int64_t zero_words;
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
@@ -314,14 +318,17 @@ int rt_similarity_f32(const float* u, const float* v, int64_t b, int d, float in
  *   (sqrt(Σ_t sumsq[t]) + 1e-6)); then torch.optim.Adam with L2 weight decay and
  *   bias correction on g·coef. The step count and learning rate are read from
  *   device memory when step_dev / lr_dev are non-NULL (hipGraph replay), else
- *   from `step` / `lr`.
+ *   from `step` / `lr`. The grads are CONSUMED: every element is zeroed after
+ *   use, and zero_buf[0, zero_words) (fp64, may be NULL) is zeroed too — the
+ *   next step's accumulators start at zero without memset launches.
  * ------------------------------------------------------------------------ */
 int rt_grad_sqnorm(const float* grads, const int64_t* offsets, int n_tensors, double* sumsq_out,
                    int32_t* step_counter, int64_t* seed_counter, void* stream);
-int rt_clip_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+int rt_clip_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq,
                       int64_t n, const double* sumsq, int n_tensors, float max_norm, float lr,
                       const float* lr_dev, float beta1, float beta2, float eps, float weight_decay,
-                      int step, const int32_t* step_dev, void* stream);
+                      int step, const int32_t* step_dev, double* zero_buf, int64_t zero_words,
+                      void* stream);
 
 /* ------------------------------------------------------------------------
  * Offline evaluation (scripts/evaluate_model.py:162-234, src/evaluation/

@@ -120,6 +120,8 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
     const int64_t row0 = static_cast<int64_t>(bid) * FM;
     const int64_t m = a.m;
+    if (blockIdx.x == 0 && a.zero_buf)
+        for (int64_t e = tid; e < a.zero_words; e += 256) a.zero_buf[e] = 0.0;
 
     // BatchNorm of the previous block: this block's batch is its row segment;
     // block 0 derives every segment (it owns the save/running-stat writes,

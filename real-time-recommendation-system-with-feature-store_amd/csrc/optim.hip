@@ -36,12 +36,13 @@ __global__ __launch_bounds__(256) void grad_sqnorm_kernel(const float* __restric
     if (threadIdx.x == 0) atomicAdd(&out[t], red[0] + red[1] + red[2] + red[3]);
 }
 
-__global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v, int64_t n,
                                                         const double* __restrict__ sumsq, int n_tensors,
                                                         float max_norm, float lr, const float* lr_dev, float b1,
                                                         float b2, float eps, float wd, int step,
-                                                        const int32_t* step_dev) {
+                                                        const int32_t* step_dev, double* __restrict__ zbuf,
+                                                        int64_t zwords) {
     __shared__ float coef_s, step_size_s, bc2_sqrt_s;
     if (threadIdx.x == 0) {
         double tot = 0.0;
@@ -69,7 +70,9 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, c
         m[e] = mv;
         v[e] = vv;
         p[e] = pv - step_size * (mv / denom);
+        g[e] = 0.f;  // consumed: the next step accumulates from zero
     }
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < zwords; e += stride) zbuf[e] = 0.0;
 }
 
 }  // namespace optim
@@ -89,17 +92,18 @@ extern "C" int rt_grad_sqnorm(const float* grads, const int64_t* offsets, int n_
     return check_launch("grad_sqnorm_kernel");
 }
 
-extern "C" int rt_clip_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+extern "C" int rt_clip_adam_step(float* params, float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                                  const double* sumsq, int n_tensors, float max_norm, float lr, const float* lr_dev,
                                  float beta1, float beta2, float eps, float weight_decay, int step,
-                                 const int32_t* step_dev, void* stream) {
+                                 const int32_t* step_dev, double* zero_buf, int64_t zero_words, void* stream) {
     if (n < 0 || !params || !grads || !exp_avg || !exp_avg_sq || !sumsq || n_tensors <= 0) return RT_ERR_INVALID;
     if (!step_dev && step < 1) return RT_ERR_INVALID;
+    if (zero_words < 0 || (zero_words > 0 && !zero_buf)) return RT_ERR_INVALID;
     if (n == 0) return RT_OK;
     int64_t blocks = (n + 255) / 256;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(optim::clip_adam_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, as_stream(stream),
                        params, grads, exp_avg, exp_avg_sq, n, sumsq, n_tensors, max_norm, lr, lr_dev, beta1, beta2,
-                       eps, weight_decay, step, step_dev);
+                       eps, weight_decay, step, step_dev, zero_buf, zero_words);
     return check_launch("clip_adam_kernel");
 }

@@ -210,24 +210,34 @@ def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
                + STAT_SLOTS * sum(b.linear.out_features for b in blocks))
 
 
+def _zero_on_entry(layer, zero_buf: Optional[torch.Tensor]):
+    """The launch clears ``zero_buf`` (fp64) before its own work (rt_linear_fwd_args.zero_buf)."""
+    if zero_buf is not None:
+        layer.zero_buf = zero_buf.data_ptr()
+        layer.zero_words = zero_buf.numel()
+
+
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
                   normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
-                  stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0) -> ChainCtx:
+                  stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0,
+                  zero_buf: Optional[torch.Tensor] = None) -> ChainCtx:
     """Run the block chain (see ``_forward_plan`` for the arguments)."""
     ctx, layers = _forward_plan(blocks, src, ids, normalize, seed_offset, stats_arena, seg_split)
+    _zero_on_entry(layers[0], zero_buf)
     st = _stream(src)
     for a in layers:
         _launch_fwd([a], st)
     return ctx
 
 
-def chain_forward_pair(first: tuple, second: tuple) -> tuple:
+def chain_forward_pair(first: tuple, second: tuple, zero_buf: Optional[torch.Tensor] = None) -> tuple:
     """Two independent chains (e.g. the item and the user tower), each given as
     the ``chain_forward`` positional arguments; layer l of both runs as ONE
     launch (``rt_linear_fwd_f32_multi``) when the chains have the same depth.
-    Returns the two ChainCtx."""
+    ``zero_buf`` is cleared by the first launch. Returns the two ChainCtx."""
     c1, l1 = _forward_plan(*first)
     c2, l2 = _forward_plan(*second)
+    _zero_on_entry(l1[0], zero_buf)
     st = _stream(first[1])
     if len(l1) == len(l2):
         for a, b in zip(l1, l2):

@@ -49,7 +49,7 @@ class LinearFwdArgs(ctypes.Structure):
         ("running_mean", vp), ("running_var", vp), ("save_mean", vp), ("save_invstd", vp),
         ("bn_eps", c_f32), ("bn_momentum", c_f32), ("drop_p", c_f32), ("drop_seed", c_u64),
         ("seed_offset", vp), ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
-        ("num_batches_tracked", vp), ("seg_split", c_i64),
+        ("num_batches_tracked", vp), ("seg_split", c_i64), ("zero_buf", vp), ("zero_words", c_i64),
     ]
 
 
@@ -97,7 +97,7 @@ SIGNATURES = {
     "rt_similarity_f32": (c_int, [vp, vp, c_i64, c_int, c_f32, vp, vp, vp, vp]),
     "rt_grad_sqnorm": (c_int, [vp, vp, c_int, vp, vp, vp, vp]),
     "rt_clip_adam_step": (c_int, [vp, vp, vp, vp, c_i64, vp, c_int, c_f32, c_f32, vp, c_f32, c_f32, c_f32,
-                                  c_f32, c_int, vp, vp]),
+                                  c_f32, c_int, vp, vp, c_i64, vp]),
     "rt_l2_augment_f32": (c_int, [vp, c_i64, c_int, vp, c_int, c_int, vp]),
     "rt_l2_finish_f32": (c_int, [vp, c_int, vp, c_int, c_int, c_i64, c_int, vp, vp, c_i64, vp]),
     "rt_exclusion_bitmap": (c_int, [vp, vp, c_i64, vp, c_i64, c_i64, vp, c_i64, vp]),

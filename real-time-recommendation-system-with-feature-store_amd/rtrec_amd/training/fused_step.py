@@ -51,17 +51,23 @@ class FusedTrainStep:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr_dev = torch.tensor([lr], dtype=torch.float32, device=dev)
         self.seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # dropout mask counter
-        # ONE fp64 arena zeroed per step: BN sums of the 3 tower calls (fwd + bwd),
-        # the loss triple and the per-tensor grad norms
+        # fp64 accumulators, cleared without memset launches: the BN column sums of
+        # the 3 tower calls (fwd + bwd) and the dbias slots live in ``arena``, which
+        # clip+Adam zeroes as the step's last launch (with the grads it consumes);
+        # the loss triple and the per-tensor grad norms live in ``small``, which the
+        # step's first forward launch zeroes (the host reads the loss after a step)
         ua = stats_arena_size(blocks_from_sequential(model.user_tower.mlp))
         ia = stats_arena_size(blocks_from_sequential(model.item_tower.mlp))
-        self._arena_sizes = [ua, ia, ia, ua, ia, ia, 3, len(self.slab.params)]
+        self._arena_sizes = [ua, ia, ia, ua, ia, ia]
         self.arena = torch.zeros(sum(self._arena_sizes), dtype=torch.float64, device=dev)
         parts, off = [], 0
         for sz in self._arena_sizes:
             parts.append(self.arena[off:off + sz])
             off += sz
-        (self.a_uf, self.a_pf, self.a_nf, self.a_ub, self.a_pb, self.a_nb, self.loss_buf, self.sumsq) = parts
+        (self.a_uf, self.a_pf, self.a_nf, self.a_ub, self.a_pb, self.a_nb) = parts
+        self.small = torch.zeros(3 + len(self.slab.params), dtype=torch.float64, device=dev)
+        self.loss_buf, self.sumsq = self.small[:3], self.small[3:]
+        self.slab.grad.zero_()  # the step owns the grad slab from here on (consumed by clip+Adam)
         # the pos and neg arenas are adjacent: together they are the [2]-segment
         # arena of the merged item chain
         self.a_pqf = self.arena[ua:ua + 2 * ia]
@@ -128,9 +134,7 @@ class FusedTrainStep:
         ib = blocks_from_sequential(m.item_tower.mlp)
         slab = self.slab
         st = native.stream_of(slab.data)
-        slab.grad.zero_()
-        self.arena.zero_()
-        so = self.seed_dev
+        so = self.seed_dev  # grads / arena are zero here (previous clip+Adam); loss / norms: first launch
         main = torch.cuda.current_stream(self.dev)
         s_u, s_p = self.side if self.concurrent else (main, main)
         b = user_ids.numel() if user_ids is not None else user_src.shape[0]
@@ -148,10 +152,10 @@ class FusedTrainStep:
                 item_src, item_ids = torch.cat([pos_src, neg_src]), None
             # user tower and merged item tower: layer l of both in ONE launch
             pq, u = chain_forward_pair((ib, item_src, item_ids, True, so, self.a_pqf, b),
-                                       (ub, user_src, user_ids, True, so, self.a_uf, 0))
+                                       (ub, user_src, user_ids, True, so, self.a_uf, 0), zero_buf=self.small)
             p_out, q_out = pq.out[:b], pq.out[b:]
         else:
-            p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf)
+            p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf, zero_buf=self.small)
             q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
                 if (neg_src is not None) else None
             p_out, q_out = p.out, (q.out if q is not None else None)
@@ -210,7 +214,7 @@ class FusedTrainStep:
                  ptr(self.step_dev), ptr(self.seed_dev), st)
             call("rt_clip_adam_step", ptr(slab.data), ptr(slab.grad), ptr(self.exp_avg), ptr(self.exp_avg_sq),
                  slab.data.numel(), ptr(self.sumsq), len(slab.params), self.max_norm, self.lr, ptr(self.lr_dev),
-                 self.b1, self.b2, self.eps, self.wd, 1, ptr(self.step_dev), st)
+                 self.b1, self.b2, self.eps, self.wd, 1, ptr(self.step_dev), ptr(self.arena), self.arena.numel(), st)
         return self.loss_buf
 
     def __call__(self, user_src: torch.Tensor, pos_src: torch.Tensor, neg_src: Optional[torch.Tensor],
