@@ -385,6 +385,56 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
             "scaling": "strong (fixed 1M-row corpus)"}
 
 
+def c5_sharded_step(dev, dist, rank, world, reps=10):
+    """C5 leg (SURVEY §8(e) training row), run collectively on every rank: a
+    100M-row x 256 bf16 item table row-sharded 12.5M rows (6.4 GB) per GPU
+    (weak scaling: the shard and the per-rank batch stay fixed as N grows, the
+    table holds 12.5M·N rows), 8,192 users per rank with uniform global positive
+    ids. One step = the owner-segment row exchange (id all-gather, owners gather
+    their rows, segment all-gather, permutation gather;
+    rtrec_amd/dist/sharded.py::sharded_gather_rows) + the 16-bit in-batch CE
+    forward+backward of the rank's users against ALL gathered rows + the loss and
+    item-gradient all-reduces (sharded_inbatch_step). time = max over ranks."""
+    from rtrec_amd.dist.sharded import sharded_inbatch_step
+    rows_per, dim, b, tau = 12_500_000, 256, 8192, 0.05
+    g = torch.Generator(device=dev).manual_seed(2000 + rank)
+    shard = torch.randn(rows_per, dim, device=dev, generator=g, dtype=torch.bfloat16) * 0.01
+    row_begin = rank * rows_per
+    gi = torch.Generator(device=dev).manual_seed(3000 + rank)
+    ids = torch.randint(0, rows_per * world, (b,), device=dev, generator=gi)
+    u = torch.nn.functional.normalize(torch.randn(b, dim, device=dev, generator=gi), dim=1).to(torch.bfloat16)
+    grp = dist.group.WORLD if dist is not None else None
+
+    def run():
+        return sharded_inbatch_step(shard, row_begin, u, ids, tau, grp)
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    run()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        loss, _, _ = run()
+    sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    out = {"ms_per_step": 1e3 * el / reps, "n_gpus": world, "table_rows": rows_per * world, "shard_rows": rows_per,
+           "emb_dim": dim, "users_per_rank": b, "dtype": "bf16", "loss": float(loss[0].item()),
+           "pairs_per_s": world * b * (b * world) * reps / el,
+           "exchange": "id all-gather + owner-segment all-gather (+ loss/grad all-reduce)",
+           "scaling": "weak (fixed shard and batch per GPU)"}
+    del shard
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -511,12 +561,16 @@ def main():
                    "parallelism": f"dp{world}", "final_loss": final_loss},
         "roofline": roof,
     }
-    scaling = None
+    scaling = c5 = None
     if not args.no_extras:  # collective: every rank
         try:
             scaling = topk_c4_scaling(dev, dist, rank, world)
         except Exception as e:  # extras never hide the headline
             scaling = {"error": repr(e)}
+        try:
+            c5 = c5_sharded_step(dev, dist, rank, world)
+        except Exception as e:
+            c5 = {"error": repr(e)}
     if rank == 0 and world == 1:
         if not args.no_extras:
             try:
@@ -537,6 +591,8 @@ def main():
                     ex["topk_c3"]["vs_cpu"] = ex["topk_c3"]["qps"] / result["cpu_baseline"]["topk"]["topk_c3"]["qps"]
             except Exception as e:
                 result["cpu_baseline"]["topk"] = {"error": repr(e)}
+    if c5 is not None:
+        result.setdefault("extras", {})["c5_sharded_step"] = c5
     if scaling is not None:
         result.setdefault("extras", {})["topk_c4_1m_sharded"] = scaling
         cb = result.get("cpu_baseline", {}).get("topk", {}).get("topk_c4")

@@ -300,13 +300,15 @@ int launch_cfg(const Args& a, const Plan& p, hipStream_t st) {
 
 #include "topk_v1.h"
 #include "topk_v2.h"
+#include "topk_v3.h"
 
 namespace rt {
 namespace topk {
 
 // kernel choice: register lists (this file) for fp32 with k <= 32; the
-// radix-compacted candidate-buffer kernel (topk_v2.h) for every dtype with
-// k <= 128 otherwise; the sorted candidate-buffer kernel (topk_v1.h) above.
+// radix-compacted candidate-buffer kernels for k <= 128 otherwise — topk_v3.h
+// for 16-bit d <= 128 (the C4 shape), topk_v2.h for fp32 and 16-bit d > 128;
+// the sorted candidate-buffer kernel (topk_v1.h) above.
 // Returns K for the list kernel, 0 for v1, -2 for v2.
 inline int list_k(bool f32, int k) {
     if (f32 && k <= 16) return 16;  // small fp32 queries: per-lane register lists (C3, serving)
@@ -330,7 +332,10 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
         }
     }
     if constexpr (v2_fits<T, S>()) {
-        if (list_k(F32, a.k) == -2) return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+        if (list_k(F32, a.k) == -2) {
+            if constexpr (!F32 && S <= 8) return v3::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+            else return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+        }
     }
     return v1::launch_S<T, S>(a, p.cap, p.splits, p.items_per_split, st);
 }

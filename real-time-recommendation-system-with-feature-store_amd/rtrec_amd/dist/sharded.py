@@ -12,9 +12,9 @@
   the whole corpus.
 * Table-sharded row gather (config C5): the owner of row ``id`` is the rank
   whose contiguous range holds it; the batch ids are all-gathered, every rank
-  gathers the rows it owns into a dense buffer (zeros elsewhere, via
-  ``rt_gather_rows``' row window) and one all-reduce(sum) leaves every row on
-  every rank.
+  gathers the rows it owns (in batch order) into one segment, the segments are
+  all-gathered and a permutation gather puts every row in batch order on every
+  rank (copies only).
 * Data-parallel in-batch step of config C5 (:func:`sharded_inbatch_step`):
   each rank scores its own users against the whole gathered batch of items.
 * Data-parallel training: the flat fp32 grad slab is averaged with one
@@ -126,28 +126,53 @@ def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Te
     """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL
     batch (all ranks' ``ids`` concatenated in rank order) on every rank.
 
-    ``gather(table, ids, row_begin)`` must return [len(ids), dim] with zero rows
-    for ids outside this rank's window (``rt_gather_rows`` semantics, the
-    default); the all-reduce(sum) then completes every row exactly once
-    (x + 0 is exact, so the result is bit-identical to a single-table gather)."""
+    Owner-segment exchange: one all-gather of (count, window) metadata and one
+    of the batch ids; every rank gathers the rows IT owns, in batch order, into
+    a segment padded to the largest owner's count; one all-gather of those
+    segments and a permutation gather (segment of owner o, slot = rank of the
+    position among o's positions) put the rows in batch order. Every row moves
+    once per receiving rank and is copied, never summed, so the result is
+    bit-identical to a single-table gather. ``gather(table, ids, row_begin)``
+    returns [len(ids), dim] (``rt_gather_rows`` semantics, the default)."""
     gather = gather or (lambda t, i, b: kernels.gather_rows(t, i, row_begin=b))
-    world, _ = _world(group)
+    world, rank = _world(group)
     if world == 1:
         return gather(table_shard, ids, row_begin)
-    n_local = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
-    counts = [torch.zeros_like(n_local) for _ in range(world)]
-    dist.all_gather(counts, n_local, group=group)
-    counts = [int(c.item()) for c in counts]
+    dev = ids.device
+    meta = torch.tensor([ids.numel(), int(row_begin), int(row_begin) + table_shard.shape[0]], dtype=torch.int64,
+                        device=dev)
+    all_meta = torch.empty(world * 3, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(all_meta, meta, group=group)
+    all_meta = all_meta.view(world, 3)
+    counts = [int(c) for c in all_meta[:, 0].tolist()]
     width = max(counts)
-    padded = torch.full((width,), -1, dtype=torch.int64, device=ids.device)
+    if width == 0:
+        return torch.empty((0, table_shard.shape[1]), dtype=table_shard.dtype, device=table_shard.device)
+    padded = torch.full((width,), -1, dtype=torch.int64, device=dev)
     padded[: ids.numel()] = ids.to(torch.int64)
-    all_ids = torch.empty((world * width,), dtype=torch.int64, device=ids.device)
+    all_ids = torch.empty((world * width,), dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(all_ids, padded, group=group)
-    keep = torch.cat([torch.arange(r * width, r * width + c, device=ids.device) for r, c in enumerate(counts)])
+    keep = torch.cat([torch.arange(r * width, r * width + c, device=dev) for r, c in enumerate(counts)])
     global_ids = all_ids[keep]
-    rows = gather(table_shard, global_ids, row_begin)
-    dist.all_reduce(rows, op=dist.ReduceOp.SUM, group=group)
-    return rows
+    # owner of each position: the rank whose [begin, end) window holds the id
+    begins = all_meta[:, 1].contiguous()
+    owner = torch.searchsorted(begins, global_ids, right=True) - 1
+    bad = (owner < 0) | (global_ids >= all_meta[owner.clamp(min=0), 2])
+    if bool(bad.any()):
+        raise IndexError("batch id outside every rank's table window")
+    per_owner = torch.bincount(owner, minlength=world)
+    seg = int(per_owner.max())
+    send = torch.zeros((seg, table_shard.shape[1]), dtype=table_shard.dtype, device=table_shard.device)
+    mine = torch.nonzero(owner == rank).flatten()
+    if mine.numel():
+        send[: mine.numel()] = gather(table_shard, global_ids[mine], row_begin)
+    segs = torch.empty((world * seg, table_shard.shape[1]), dtype=table_shard.dtype, device=table_shard.device)
+    dist.all_gather_into_tensor(segs, send, group=group)
+    order = torch.argsort(owner, stable=True)
+    starts = torch.cumsum(per_owner, 0) - per_owner
+    slot = torch.empty_like(owner)
+    slot[order] = torch.arange(owner.numel(), device=dev) - starts[owner[order]]
+    return gather(segs, owner * seg + slot, 0)
 
 
 def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: torch.Tensor,

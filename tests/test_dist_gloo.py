@@ -127,11 +127,12 @@ def test_sharded_topk_query_owner_gloo(world, n, k):
     _run(world, _topk_owner_worker, n, 32, 24, k, 11)
 
 
-def _gather_worker(rank, world, n, d, seed):
+def _gather_worker(rank, world, n, d, seed, counts, skew):
     rng = np.random.default_rng(seed)
     table = rng.standard_normal((n, d)).astype(np.float32)
-    counts = [13, 29]
-    all_ids = [rng.integers(0, n, size=c) for c in counts]
+    # skew: every id in the first shard's window, so the other owners' segments are empty
+    hi = shard_range(n, world, 0)[1] if skew else n
+    all_ids = [rng.integers(0, hi, size=c) for c in counts]
     b, c = shard_range(n, world, rank)
     shard = torch.from_numpy(table[b:b + c])
 
@@ -147,8 +148,13 @@ def _gather_worker(rank, world, n, d, seed):
     np.testing.assert_array_equal(rows.numpy(), ref)
 
 
-def test_sharded_gather_rows_gloo():
-    _run(2, _gather_worker, 997, 16, 3)
+@pytest.mark.parametrize("world,counts,skew", [(2, [13, 29], False), (4, [7, 0, 31, 16], False),
+                                               (2, [40, 9], True), (3, [5, 5, 5], True)])
+def test_sharded_gather_rows_gloo(world, counts, skew):
+    """C5 owner-segment exchange: ragged per-rank batches (one empty), ids
+    skewed onto one owner (empty segments elsewhere): rows in batch order,
+    bit-exact."""
+    _run(world, _gather_worker, 997, 16, 3, counts, skew)
 
 
 def _dp_worker(rank, world):
