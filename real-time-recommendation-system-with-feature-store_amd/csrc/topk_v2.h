@@ -37,7 +37,10 @@ namespace v2 {
 constexpr int kWavesB = 8;            // waves per block
 constexpr int kQT = 32 * kWavesB;     // queries per block
 constexpr int kNT = 128;              // split granularity; items per LDS stage: Cfg2::NT
-constexpr int kCap = 512;             // candidate entries per query
+#ifndef RT_TOPK_CAP
+#define RT_TOPK_CAP 512
+#endif
+constexpr int kCap = RT_TOPK_CAP;     // candidate entries per query
 constexpr int kHalf = kCap / 2;       // per owning lane
 constexpr int kE = kCap / 64;         // entries per lane in a compaction
 constexpr int kMaxKv2 = 128;

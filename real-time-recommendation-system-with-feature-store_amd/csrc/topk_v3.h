@@ -20,6 +20,8 @@
 // * three-stage LDS ring: tiles are DMA'd two stages ahead.
 #pragma once
 
+#include <type_traits>
+
 namespace rt {
 namespace topk {
 namespace v3 {
@@ -55,10 +57,18 @@ struct Cfg3 {
     static constexpr int TILE_BYTES = SLOTS * 16;
     static_assert(PIECES * 64 == SLOTS, "whole DMA pieces");
 };
+#ifndef RT_TOPK3_PREF_K
+#define RT_TOPK3_PREF_K 0
+#endif
+constexpr int kPrefilterK = RT_TOPK3_PREF_K;
+#ifndef RT_TOPK3_LIMK
+#define RT_TOPK3_LIMK 2
+#endif
+constexpr int kRefreshMul = RT_TOPK3_LIMK;
 constexpr int kRing = RT_TOPK3_RING;  // LDS ring depth: 2 (DMA one stage ahead) or 3 (two)
-static_assert(kRing == 2 || kRing == 3, "VMEM bookkeeping covers rings of 2 or 3 stages");
+static_assert(kRing >= 2 && kRing <= 4, "ring of 2..4 stages");
 
-template <typename T, int S, bool EXCL>
+template <typename T, int S, bool EXCL, bool PREF>
 __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits, int64_t items_per_split) {
     using M = Mfma<T>;
     using C = Cfg3<T, S>;
@@ -113,8 +123,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
     const uint64_t wbase = (static_cast<uint64_t>(wb_hi) << 32) | wb_lo;
     const uint32_t woff0 = static_cast<uint32_t>((col * kCap + half * kHalf) * sizeof(Cand));
     uint32_t woff = woff0;
-    // checked once per stage: room for a whole stage's appends (16 rows per sub-tile)
-    const uint32_t woff_lim = woff0 + static_cast<uint32_t>((kHalf - C::NSUB * 16) * sizeof(Cand));
+    // checked once per stage: room for a whole stage's appends (16 rows per sub-tile);
+    // small k compacts early too — a half holding ~2k entries refreshes a stale threshold
+    const int lim_n = kRefreshMul > 0 ? min(kHalf - C::NSUB * 16, kRefreshMul * k + 32) : kHalf - C::NSUB * 16;
+    const uint32_t woff_lim = woff0 + static_cast<uint32_t>(lim_n * sizeof(Cand));
 
     // ---- DMA plan: this wave's pieces w, w+8, ... of a stage ----
     // SADDR form: source = the stage's first row (uniform, SGPRs) + a 32-bit
@@ -132,7 +144,15 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         soff[i] = static_cast<uint32_t>(r * static_cast<int>(row_bytes) + (c < row_vecs ? c * 16 : 0));
     }
     const uint32_t tile0 = lds_addr(&tile[0][0]);
-    int vm_old = 0, vm_new = 0;  // as in v2: VMEM ops younger than the awaited / the youngest DMA
+    // VMEM bookkeeping (wave-uniform): `issued` counts this wave's vector-memory
+    // operations; mk[j] = the count right after the DMA of stage s+1+j was
+    // issued (mk[0]: the one the current stage's end waits for). Waiting for
+    // vmcnt <= issued - mk[0] waits for that DMA and nothing younger — never for
+    // candidate stores' acknowledgements. A drain sets every mark to `issued`.
+    int issued = 0;
+    int mk[kRing - 1];
+#pragma unroll
+    for (int j = 0; j < kRing - 1; ++j) mk[j] = 0;
     auto fetch = [&](int64_t t0, int buf) {
         const uint32_t base = tile0 + buf * C::TILE_BYTES + wave_u * 1024;
         const char* sb = Xb + t0 * row_bytes;
@@ -155,9 +175,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
                     : "memory");
             }
         }
-        if constexpr (kRing == 3) vm_old += npieces;  // younger than the DMA the current stage's end waits for
-        else vm_old = 0;                               // it is this DMA
-        vm_new = 0;
+        issued += npieces;
     };
     auto raw_barrier = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -183,8 +201,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
                 } else {
                     p = __builtin_amdgcn_inverse_ballot_w64(pm[r]);
                 }
-                vm_old += 2;
-                vm_new += 2;
+                issued += 2;
                 if (p) {
                     // id = sub0 + tile_row(r, half): a per-sub-tile lane base + an immediate
                     const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
@@ -215,7 +232,8 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
                 thr = nt;
             }
         }
-        vm_old = vm_new = 0;  // drained
+#pragma unroll
+        for (int j = 0; j < kRing - 1; ++j) mk[j] = issued;  // drained
     };
     auto select = [&](const f32x16& acc, int64_t sub0) {
         uint64_t pm[16], any = 0;
@@ -242,16 +260,42 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
     auto step = [&](const frag (&af)[S], f32x16& acc, const f32x16& prev, int64_t subp) {
         uint64_t pm[16], any = 0;
         acc = f32x16{};
-        constexpr int CPG = (16 + S - 1) / S;
+        if constexpr (PREF) {
+            // small k: a max-of-16 (v_max3 tree) and one compare in the MFMA gaps;
+            // the per-row masks only when some lane of the wave passes
+            float m = 0.f;
 #pragma unroll
-        for (int s = 0; s < S; ++s) {
-            acc = M::run(af[s], qf[s], acc);
+            for (int s = 0; s < S; ++s) {
+                acc = M::run(af[s], qf[s], acc);
+                if (s == 0) m = fmaxf(fmaxf(prev[0], prev[1]), prev[2]);
+                if (s == 1) m = fmaxf(fmaxf(m, prev[3]), prev[4]);
+                if (s == 2) m = fmaxf(fmaxf(m, prev[5]), prev[6]);
+                if (s == 3) m = fmaxf(fmaxf(m, prev[7]), prev[8]);
+                if (s == 4 || (S < 8 && s == S - 1)) {
+                    m = fmaxf(fmaxf(m, prev[9]), prev[10]);
+                    m = fmaxf(fmaxf(m, prev[11]), prev[12]);
+                    m = fmaxf(fmaxf(m, prev[13]), prev[14]);
+                    m = fmaxf(m, prev[15]);
+                }
+            }
+            if (__ballot(m >= thr) == 0) return;
 #pragma unroll
-            for (int j = 0; j < CPG; ++j) {
-                const int r = s * CPG + j;
-                if (r < 16) {
-                    pm[r] = __ballot(prev[r] >= thr);
-                    any |= pm[r];
+            for (int r = 0; r < 16; ++r) {
+                pm[r] = __ballot(prev[r] >= thr);
+                any |= pm[r];
+            }
+        } else {
+            constexpr int CPG = (16 + S - 1) / S;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                acc = M::run(af[s], qf[s], acc);
+#pragma unroll
+                for (int j = 0; j < CPG; ++j) {
+                    const int r = s * CPG + j;
+                    if (r < 16) {
+                        pm[r] = __ballot(prev[r] >= thr);
+                        any |= pm[r];
+                    }
                 }
             }
         }
@@ -266,12 +310,17 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         }
     };
 
-    // prologue: stages 0 and 1 in flight, both landed
-    if (i_begin < i_end) fetch(i_begin, 0);
-    if (kRing == 3 && i_begin + C::NT < i_end) fetch(i_begin + C::NT, 1);
-    wait_vm_le(0);
-    vm_old = vm_new = 0;
+    // prologue: stages 0 .. kRing-2 in flight, stage 0 landed
+    int mark0 = 0;
+#pragma unroll
+    for (int b = 0; b < kRing - 1; ++b) {
+        if (i_begin + b * C::NT < i_end) fetch(i_begin + b * C::NT, b);
+        if (b == 0) mark0 = issued;
+        else mk[b - 1] = issued;
+    }
+    wait_vm_le(issued - mark0);
     raw_barrier();
+    RT_PT(uint64_t pc_wait = 0, pc_bar = 0, pc_steps = 0, pc_cmp = 0; const uint64_t pc_start = clock64();)
 
     frag af[S];  // one set: sub-tile t+1's reads refill each fragment once t's MFMA on it has issued
     f32x16 accA, accB;
@@ -285,8 +334,11 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         const bool more = t0 + C::NT < i_end;
         const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);  // rows in this stage
         if (t0 + (kRing - 1) * C::NT < i_end) fetch(t0 + (kRing - 1) * C::NT, cur == 0 ? kRing - 1 : cur - 1);
+        mk[kRing - 2] = issued;
         const char* stage = &tile[cur][0] + a_lane;
+        RT_PT(const uint64_t c4s = clock64();)
         maybe_compact();  // the only call site in the loop (keeps the call's register saves out of the steps)
+        RT_PT(const uint64_t c5s = clock64(); pc_cmp += c5s - c4s;)
         // sub-tiles in accumulators A, B, A, B, ... (the previous stage ended on B);
         // each sub-tile's A fragments are read while the one before computes
 #pragma unroll
@@ -307,9 +359,13 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
                 }
             }
         }
-        if (more) wait_vm_le(vm_old);  // the next stage's DMA has landed
+        RT_PT(const uint64_t c6 = clock64(); pc_steps += c6 - c5s;)
+        if (more) wait_vm_le(issued - mk[0]);  // the next stage's DMA has landed
+        RT_PT(const uint64_t c7 = clock64(); pc_wait += c7 - c6;)
         raw_barrier();
-        vm_old = vm_new;
+        RT_PT(pc_bar += clock64() - c7;)
+#pragma unroll
+        for (int j = 0; j + 1 < kRing - 1; ++j) mk[j] = mk[j + 1];
         cur = cur == kRing - 1 ? 0 : cur + 1;
         if (more) lds_a(af, &tile[cur][0] + a_lane, 0);
     }
@@ -319,37 +375,91 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         maybe_compact();
     }
 
+    RT_PT(const uint64_t c4 = clock64();)
     // ---- final selection, one query of the wave at a time (as v2) ----
     __threadfence_block();
     float* os = a.out_s + static_cast<int64_t>(split) * nq * k;
     int64_t* oi = a.out_i + static_cast<int64_t>(split) * nq * k;
-    for (int c = 0; c < 32; ++c) {
+    // one query of the wave at a time; a query whose buffer holds <= 128 entries
+    // (the common case) is sorted from registers loaded while the previous query
+    // sorted, so the global-load latency is paid once, not 32 times
+    const int cnt_all = static_cast<int>((woff - woff0) / sizeof(Cand));
+    auto load2 = [&](int c, float (&sv)[2], uint32_t (&iv)[2]) {
+        const Cand* b = cbase + static_cast<int64_t>(c) * kCap;
+        const int n0 = __shfl(cnt_all, c, 64), n1 = __shfl(cnt_all, c + 32, 64);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int r = lane * 2 + j;
+            const Cand e = r < n0 + n1 ? v2::entry(b, n0, r) : Cand{-INFINITY, kEmptyId};
+            sv[j] = e.s;
+            iv[j] = e.i;
+        }
+    };
+    float sn[2];
+    uint32_t in[2];
+    const int nvalid = static_cast<int>(nq - qw < 32 ? (nq - qw > 0 ? nq - qw : 0) : 32);
+    if (nvalid > 0) load2(0, sn, in);
+    for (int c = 0; c < nvalid; ++c) {
         const int64_t gq = qw + c;
-        if (gq >= nq) break;
-        Cand* b = cbase + static_cast<int64_t>(c) * kCap;
-        const int cnt = static_cast<int>((woff - woff0) / sizeof(Cand));
-        int n0 = __shfl(cnt, c, 64), n1 = __shfl(cnt, c + 32, 64);
-        if (n0 + n1 > 128) {
+        float sc[2] = {sn[0], sn[1]};
+        uint32_t ic[2] = {in[0], in[1]};
+        if (c + 1 < nvalid) load2(c + 1, sn, in);  // in flight during this query's sort
+        int n0 = __shfl(cnt_all, c, 64), n1 = __shfl(cnt_all, c + 32, 64);
+        float* orow = os + gq * k;
+        int64_t* irow = oi + gq * k;
+        if (n0 + n1 <= 128) {
+            wave_sort_regs<2>(sc, ic);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int r = lane * 2 + j;
+                if (r < k) {
+                    const bool ok = ic[j] != kEmptyId;
+                    orow[r] = ok ? sc[j] : -FLT_MAX;
+                    irow[r] = ok ? static_cast<int64_t>(ic[j]) + a.id_offset : -1;
+                }
+            }
+        } else {
+            Cand* b = cbase + static_cast<int64_t>(c) * kCap;
             float nt;
             const int nn = compact_query(b, n0, n1, k, whist, nt);
             n0 = (nn + 1) >> 1;
             n1 = nn >> 1;
+            if (n0 + n1 <= 128) emit_sorted<2>(b, n0, n1, k, orow, irow, a.id_offset);
+            else emit_sorted<kE>(b, n0, n1, k, orow, irow, a.id_offset);
         }
-        if (n0 + n1 <= 128) emit_sorted<2>(b, n0, n1, k, os + gq * k, oi + gq * k, a.id_offset);
-        else emit_sorted<kE>(b, n0, n1, k, os + gq * k, oi + gq * k, a.id_offset);
     }
+#ifdef RT_TOPK_PROBE_TIMING
+    {
+        const uint64_t c5 = clock64();
+        const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesB + wave;
+        if (lane == 0 && gw < 65536) {
+            uint64_t* o = v2::probe_cycles + gw * 6;
+            o[0] = c5 - pc_start; o[1] = pc_wait; o[2] = pc_bar; o[3] = pc_steps; o[4] = pc_cmp; o[5] = c5 - c4;
+        }
+    }
+#endif
 }
 
 template <typename T, int S>
 int launch_S(const Args& a, int splits, int64_t items_per_split, hipStream_t st) {
     const int64_t q_tiles = (a.nq + kQT - 1) / kQT;
     dim3 grid(static_cast<unsigned>(q_tiles * splits));
-    if (a.excl)
-        hipLaunchKernelGGL((flatip_topk_v3_kernel<T, S, true>), grid, dim3(64 * kWavesB), 0, st, a, splits,
-                           items_per_split);
-    else
-        hipLaunchKernelGGL((flatip_topk_v3_kernel<T, S, false>), grid, dim3(64 * kWavesB), 0, st, a, splits,
-                           items_per_split);
+    // small k: the max-of-16 prefilter (most sub-tiles pass no lane); large k:
+    // per-row compares straight away (nearly every sub-tile has a passing row)
+    const bool pref = a.k < kPrefilterK;
+    auto go = [&](auto ex, auto pf) {
+        hipLaunchKernelGGL((flatip_topk_v3_kernel<T, S, decltype(ex)::value, decltype(pf)::value>), grid,
+                           dim3(64 * kWavesB), 0, st, a, splits, items_per_split);
+    };
+    using TT = std::true_type;
+    using FF = std::false_type;
+    if (a.excl) {
+        if (pref) go(TT{}, TT{});
+        else go(TT{}, FF{});
+    } else {
+        if (pref) go(FF{}, TT{});
+        else go(FF{}, FF{});
+    }
     return check_launch("flatip_topk_v3_kernel");
 }
 
