@@ -446,9 +446,10 @@ def main():
     ap.add_argument("--eager", action="store_true",
                     help="time eager steps (default: hipGraph replays of the captured step, inputs copied in)")
     args = ap.parse_args()
-    # hipGraph replay on one GPU; eager steps under data parallelism (the RCCL
-    # all-reduce between the two captured halves is not exercised off the box)
-    args.graph = not args.eager and args.gpus == 1
+    # hipGraph replay (default): one graph per step on one GPU; under data
+    # parallelism two graphs (gradients; clip+Adam) with the RCCL all-reduce of
+    # the flat grad slab launched between them (FusedTrainStep.capture)
+    args.graph = not args.eager
 
     dist, rank, world, dev = dist_setup(args.gpus)
     torch.cuda.set_device(dev)

@@ -70,3 +70,37 @@ def test_graph_capture_keeps_warmup_when_asked(device):
             dst.copy_(src)
         got.append(g.replay().clone())
     _check(m1, m2, ref[2:], got)
+
+
+def test_two_graph_data_parallel_capture(device):
+    """The data-parallel form bench.py replays at N > 1: with a process group the
+    step is captured as two graphs (gradients; clip+Adam) with the all-reduce
+    of the flat grad slab launched eagerly between them. Exercised here with a
+    one-rank gloo group (the all-reduce is then x·1): the replays equal the
+    eager single-process steps."""
+    import socket
+
+    import torch.distributed as dist
+
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        ut, mt, batches, m1 = _setup(device)
+        m2 = copy.deepcopy(m1)
+        eager = FusedTrainStep(m1)
+        ref = [eager(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone() for b in batches]
+        g = FusedTrainStep(m2, process_group=dist.group.WORLD)
+        st = tuple(t.clone() for t in batches[0])
+        g.capture(ut, mt, mt, user_ids=st[0], pos_ids=st[1], neg_ids=st[2], warmup=1)
+        assert g.graph_update is not None
+        got = []
+        for b in batches:
+            for dst, src in zip(st, b):
+                dst.copy_(src)
+            got.append(g.replay().clone())
+        _check(m1, m2, ref, got)
+    finally:
+        dist.destroy_process_group()
