@@ -31,5 +31,5 @@ Shape shape_f16(int d, int k) {
 }  // namespace rt
 
 #ifdef RT_TOPK_PROBE_TIMING
-extern "C" void* rt_topk_probe_cycles_f16() { return rt::topk::v2::probe_cycles_addr(); }
+extern "C" void* rt_topk_probe_cycles_f16() { return rt::topk::v3::probe_cycles_addr(); }
 #endif

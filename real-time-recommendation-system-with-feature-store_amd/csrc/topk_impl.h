@@ -307,8 +307,10 @@ namespace topk {
 
 // kernel choice: register lists (this file) for fp32 with k <= 32; the
 // radix-compacted candidate-buffer kernels for k <= 128 otherwise — topk_v3.h
-// for 16-bit d <= 128 (the C4 shape), topk_v2.h for fp32 and 16-bit d > 128;
-// the sorted candidate-buffer kernel (topk_v1.h) above.
+// for 16-bit d <= 128 with k <= 32 (its scan and threshold refresh win at
+// small k), topk_v2.h for the rest (fp32, d > 128, and 32 < k <= 128, where
+// v2's buffer schedule measured faster: C4 k=100 4.96 vs 5.15 ms); the sorted
+// candidate-buffer kernel (topk_v1.h) above.
 // Returns K for the list kernel, 0 for v1, -2 for v2.
 inline int list_k(bool f32, int k) {
     if (f32 && k <= 16) return 16;  // small fp32 queries: per-lane register lists (C3, serving)
@@ -333,8 +335,10 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
     }
     if constexpr (v2_fits<T, S>()) {
         if (list_k(F32, a.k) == -2) {
-            if constexpr (!F32 && S <= 8) return v3::launch_S<T, S>(a, p.splits, p.items_per_split, st);
-            else return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+            if constexpr (!F32 && S <= 8) {
+                if (a.k <= v3::kMaxKv3) return v3::launch_S<T, S>(a, p.splits, p.items_per_split, st);
+            }
+            return v2::launch_S<T, S>(a, p.splits, p.items_per_split, st);
         }
     }
     return v1::launch_S<T, S>(a, p.cap, p.splits, p.items_per_split, st);

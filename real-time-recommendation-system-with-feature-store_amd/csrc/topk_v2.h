@@ -37,30 +37,10 @@ namespace v2 {
 constexpr int kWavesB = 8;            // waves per block
 constexpr int kQT = 32 * kWavesB;     // queries per block
 constexpr int kNT = 128;              // split granularity; items per LDS stage: Cfg2::NT
-#ifndef RT_TOPK_CAP
-#define RT_TOPK_CAP 512
-#endif
-constexpr int kCap = RT_TOPK_CAP;     // candidate entries per query
+constexpr int kCap = 512;             // candidate entries per query
 constexpr int kHalf = kCap / 2;       // per owning lane
 constexpr int kE = kCap / 64;         // entries per lane in a compaction
 constexpr int kMaxKv2 = 128;
-#ifndef RT_TOPK_NBUF
-#define RT_TOPK_NBUF 3
-#endif
-#ifdef RT_TOPK_PROBE_TIMING
-// probe builds only: per-wave cycle attribution [total, DMA wait, barrier, appends, compaction, final]
-__device__ uint64_t probe_cycles[65536 * 6];
-inline void* probe_cycles_addr() {
-    void* p = nullptr;
-    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(probe_cycles));
-    return p;
-}
-#define RT_PT(...) __VA_ARGS__
-#else
-#define RT_PT(...)
-#endif
-constexpr int kNBuf = RT_TOPK_NBUF;  // LDS ring depth: item tiles kNBuf-1 stages ahead (MALL latency)
-static_assert(kNBuf == 2 || kNBuf == 3, "VMEM bookkeeping covers rings of 2 or 3 tiles");
 
 // order-preserving key of a score; -0 is folded onto +0 (they compare equal)
 __device__ __forceinline__ uint32_t okey(float s) {
@@ -208,23 +188,16 @@ __device__ __noinline__ void emit_sorted(const Cand* __restrict__ buf, int n0, i
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // wait until at most n (wave-uniform, >= 0) vector-memory operations are in
-// flight — exactly n (capped at the counter's 63): a bound rounded down would
-// also wait for the youngest candidate stores' acknowledgements
-template <int N>
-__device__ __forceinline__ void wait_vm_exact() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+// flight, rounded down to a power of two
+__device__ __forceinline__ void wait_vm_le(int n) {
+    if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-template <int LO, int HI>
-__device__ __forceinline__ void wait_vm_range(int n) {
-    if constexpr (LO == HI) {
-        wait_vm_exact<LO>();
-    } else {
-        constexpr int MID = (LO + HI) / 2;
-        if (n <= MID) wait_vm_range<LO, MID>(n);
-        else wait_vm_range<MID + 1, HI>(n);
-    }
-}
-__device__ __forceinline__ void wait_vm_le(int n) { wait_vm_range<0, 63>(n > 63 ? 63 : n); }
 
 template <typename T, int S>
 struct Cfg2 {
@@ -264,8 +237,9 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     using M = Mfma<T>;
     using C = Cfg2<T, S>;
     constexpr int DP = C::DP, VEC = C::VEC, ROWB = C::ROWB;
-    __shared__ __attribute__((aligned(1024))) T tile[kNBuf][C::TILE_BYTES / sizeof(T)];
+    __shared__ __attribute__((aligned(1024))) T tile[2][C::TILE_BYTES / sizeof(T)];
     __shared__ __attribute__((aligned(16))) uint32_t hist[kWavesB][256];
+    __shared__ __attribute__((aligned(16))) float scr[kWavesB * 64 * 20];  // per-lane score rows (80 B: conflict-free b128)
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
     const T* __restrict__ X = reinterpret_cast<const T*>(a.X);
@@ -282,7 +256,9 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     const int row_vecs = d / VEC;
     const int64_t q_pad = static_cast<int64_t>(gridDim.x / splits) * kQT;  // buffers per split
     Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32 buffers
+    Cand* const mybuf = cbase + static_cast<int64_t>(col) * kCap + half * kHalf;  // this lane's half
     uint32_t* const whist = hist[wave];
+    float* const wscr = scr + (wave * 64 + lane) * 20;
 
     typename M::frag qf[S];
     {
@@ -307,37 +283,11 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
     }
     const uint32_t* excl = (EXCL && qok) ? a.excl + q * a.excl_words : nullptr;
     float thr = qok ? -FLT_MAX : INFINITY;
-#ifdef RT_TOPK_PROBE_NOSEL
-    thr = INFINITY;  // probe builds only (tools/hip_probe/topk_probe.hip): the scan without selection
-#endif
-    // append cursor: byte offset of the lane's next entry from the wave's
-    // (uniform) buffer base, so a store is SADDR + one 32-bit VGPR
-    // (readfirstlane returns int: take each half as uint32_t before widening, or a
-    // low word with bit 31 set sign-extends over the high word)
-    const uint32_t wb_lo = static_cast<uint32_t>(
-        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase))));
-    const uint32_t wb_hi = static_cast<uint32_t>(
-        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase) >> 32)));
-    const uint64_t wbase = (static_cast<uint64_t>(wb_hi) << 32) | wb_lo;
-    const uint32_t woff0 = static_cast<uint32_t>((col * kCap + half * kHalf) * sizeof(Cand));
-    uint32_t woff = woff0;
-    // compaction trigger per lane: a full half, or (small k) once enough entries
-    // arrived to refresh a stale threshold
-#ifndef RT_TOPK_LIM_MUL
-#define RT_TOPK_LIM_MUL 0
-#endif
-#ifndef RT_TOPK_LIM_ADD
-#define RT_TOPK_LIM_ADD 32
-#endif
-    const int lim_n = RT_TOPK_LIM_MUL > 0 ? min(kHalf - 16, RT_TOPK_LIM_MUL * k + RT_TOPK_LIM_ADD) : kHalf - 16;
-    const uint32_t woff_lim = woff0 + static_cast<uint32_t>(lim_n * sizeof(Cand));
+    int cnt = 0;
 
     // LDS-DMA of one tile (rows t0 .., zero chunks past d; rows past the split
     // end read a clamped valid row — their scores are masked to -inf)
-    // VMEM instructions issued after the DMA the end of this stage waits for
-    // (vm_old: the next stage's) and after the youngest DMA (vm_new); wave-uniform.
-    // A drain (compaction) zeroes both: then the waits are no-ops.
-    int vm_old = 0, vm_new = 0;
+    int vm_after = 0;  // VMEM instructions issued since the last DMA (wave-uniform); >= 1<<20: drained
     const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
     auto fetch = [&](int64_t t0, int buf) {
         const uint32_t base = lds_addr(&tile[buf][0]) + wave_u * (C::DMA_PER_WAVE * 1024);
@@ -352,120 +302,93 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
                                            : static_cast<const void*>(&kZero16);
             glds16(src, base + j * 1024);
         }
-        if constexpr (kNBuf == 3) vm_old += C::DMA_PER_WAVE;  // younger than the awaited DMA
-        vm_new = 0;
+        vm_after = 0;
     };
-    // the next stage's DMA has landed (every VMEM operation younger than it counted)
-    auto fetch_wait = [&]() { wait_vm_le(vm_old); };
+    // the DMA into the other buffer has landed (its count bound is exact or drained)
+    auto fetch_wait = [&]() {
+        if (vm_after < (1 << 20)) wait_vm_le(vm_after);
+    };
     auto raw_barrier = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
 
-    // Selection from one 32-item sub-tile's scores (acc[r] = item sub0 + tile_row(r, half),
-    // query col), in two parts. masks(): per score one compare into an SGPR wave
-    // mask (v_cmp → s[..], no per-lane mask building) — straight-line, so the
-    // 16-bit loop below runs it in the MFMA gaps of the next sub-tile. appends():
-    // the wave visits only the rows r some lane passes and stores those lanes'
-    // entries with two masked dword stores per row.
-    auto masks = [&](const f32x16& acc, uint64_t (&pm)[16], uint64_t& any) {
-        any = 0;
+    // select from one 32-item sub-tile's scores (acc[r] = item sub0 + tile_row(r, half), query col)
+    auto select = [&](const f32x16& acc, int64_t sub0) {
+        float m = acc[0];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            pm[r] = __ballot(acc[r] >= thr);
-            any |= pm[r];
-        }
-    };
-    auto appends = [&](const f32x16& acc, int64_t sub0, const uint64_t (&pm)[16], uint64_t any) {
-        if (!any) return;
-        uint32_t xw = 0u;
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, acc[r]);
+        if (__ballot(m >= thr) == 0) return;
+        // per-lane pass mask, 2 VALU per score: bit 15-r <=> acc[r] passes
+        uint32_t bits = 0u;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            asm("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+                : "+v"(bits)
+                : "v"(acc[r]), "v"(thr)
+                : "vcc");
         if constexpr (EXCL) {
-            if (excl) xw = excl[sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
-        }
+            if (excl) {
+                const uint32_t xw = excl[sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (pm[r]) {  // wave-uniform
-                bool p;
-                if constexpr (EXCL) {
-                    p = acc[r] >= thr && !((xw >> tile_row(r, half)) & 1u);
-                    if (!__ballot(p)) continue;
-                } else {
-                    p = __builtin_amdgcn_inverse_ballot_w64(pm[r]);  // exec = pm[r], no compare
-                }
-                vm_old += 2;  // exactly two store instructions for the wave
-                vm_new += 2;
-                if (p) {
-                    // score and id as two dword stores of one entry (SADDR form: uniform base +
-                    // 32-bit lane offset), no register moves to pair them up; the cursor
-                    // advances inside the statement (under this exec mask, in place)
-                    const uint32_t id = static_cast<uint32_t>(sub0 + tile_row(r, half));
-                    asm volatile(
-                        "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
-                        "v_add_u32 %0, 8, %0"
-                        : "+v"(woff)
-                        : "v"(acc[r]), "s"(wbase), "v"(id)
-                        : "memory");
-                }
+                for (int r = 0; r < 16; ++r)
+                    if ((xw >> tile_row(r, half)) & 1u) bits &= ~(1u << (15 - r));
+            }
+        }
+        // the lane's scores go through its LDS scratch row so the append loop
+        // can index them; the wave loops max-popcount times (1-2 late in a scan)
+        if (bits) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<float4*>(wscr + 4 * i) =
+                    make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        }
+        wave_lds_sync();
+        while (__ballot(bits != 0u)) {
+            ++vm_after;  // one store instruction for the wave
+            if (bits) {
+                const int b = 31 - __builtin_clz(bits);  // highest set bit = lowest r
+                bits &= ~(1u << b);
+                const int r = 15 - b;
+                const float v = wscr[r];
+                mybuf[cnt] = Cand{v, static_cast<uint32_t>(sub0 + tile_row(r, half))};
+                ++cnt;
             }
         }
     };
-    auto select = [&](const f32x16& acc, int64_t sub0) {
-        uint64_t pm[16], any;
-        masks(acc, pm, any);
-        appends(acc, sub0, pm, any);
-    };
     // compact every buffer of this wave that may overflow on the next sub-tile
     auto maybe_compact = [&]() {
-        const uint64_t m = __ballot(woff > woff_lim);
+        const uint64_t m = __ballot(cnt > kHalf - 16);
         uint32_t need = static_cast<uint32_t>(m) | static_cast<uint32_t>(m >> 32);
         if (!need) return;
         __threadfence_block();
         while (need) {
             const int c = __builtin_ctz(need);
             need &= need - 1;
-            const int cnt = static_cast<int>((woff - woff0) / sizeof(Cand));
             const int n0 = __shfl(cnt, c, 64), n1 = __shfl(cnt, c + 32, 64);
             float nt;
             const int nn = compact_query(cbase + static_cast<int64_t>(c) * kCap, n0, n1, k, whist, nt);
             if (col == c) {
-                woff = woff0 + static_cast<uint32_t>((half ? nn >> 1 : (nn + 1) >> 1) * sizeof(Cand));
+                cnt = half ? nn >> 1 : (nn + 1) >> 1;
                 thr = nt;
             }
         }
-        vm_old = vm_new = 0;  // the compaction drained every outstanding VMEM operation
+        vm_after = 1 << 20;  // the compaction drained every outstanding VMEM operation
     };
 
-    constexpr int NT = C::NT;
-    // prologue: stages 0 .. kNBuf-2 in flight, stage 0 landed
-#pragma unroll
-    for (int b = 0; b < kNBuf - 1; ++b)
-        if (i_begin + b * NT < i_end) fetch(i_begin + b * NT, b);
-    wait_vm_le(0);
-    vm_old = vm_new = 0;
+    if (i_begin < i_end) {
+        fetch(i_begin, 0);
+        wait_vm_le(0);
+    }
     raw_barrier();
-    RT_PT(uint64_t pc_wait = 0, pc_bar = 0, pc_app = 0, pc_cmp = 0; const uint64_t pc_start = clock64();)
     int cur = 0;
-    auto next_stage = [&]() {
-        // next stage: the DMA its end waits for is the youngest one now (kNBuf = 3);
-        // for kNBuf = 2 that DMA is issued at its top (fetch adds its count)
-        vm_old = kNBuf == 2 ? 0 : vm_new;
-        cur = cur == kNBuf - 1 ? 0 : cur + 1;
-    };
-    auto mask_tail = [&](f32x16& acc, int64_t sub0) {
-        if (sub0 + 32 > i_end) {  // rows past the end never qualify
-            const int left = static_cast<int>(i_end - sub0);
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (tile_row(r, half) >= left) acc[r] = -INFINITY;
-        }
-    };
-    // fp32, and 16-bit d > 128 (16-bit d <= 128 runs topk_v3.h)
+    constexpr int NT = C::NT;
     for (int64_t t0 = i_begin; t0 < i_end; t0 += NT) {
         const T* tl = tile[cur];
         const bool more = t0 + NT < i_end;
-        // stage + kNBuf-1 into the buffer read in the previous stage (all waves are past its barrier)
-        if (t0 + (kNBuf - 1) * NT < i_end) fetch(t0 + (kNBuf - 1) * NT, cur == 0 ? kNBuf - 1 : cur - 1);
+        // the next tile's DMA: buffer cur^1 was last read before the previous barrier
+        if (more) fetch(t0 + NT, cur ^ 1);
 #pragma unroll
         for (int rt = 0; rt < NT / 32; ++rt) {
             const int64_t sub0 = t0 + rt * 32;
@@ -485,25 +408,25 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
             } else {
                 typename M::frag af[S];
 #pragma unroll
-                for (int s = 0; s < S; ++s)
-                    af[s] = frag_from<T>(arow + ((2 * s + half) ^ C::swz(row)) * VEC);
+                for (int s = 0; s < S; ++s) af[s] = frag_from<T>(arow + ((2 * s + half) ^ C::swz(row)) * VEC);
                 __builtin_amdgcn_sched_barrier(0);  // every read in flight before the first MFMA waits
 #pragma unroll
                 for (int s = 0; s < S; ++s) acc = M::run(af[s], qf[s], acc);
             }
-            mask_tail(acc, sub0);
+            if (sub0 + 32 > i_end) {  // rows past the end never qualify
+                const int left = static_cast<int>(i_end - sub0);
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (tile_row(r, half) >= left) acc[r] = -INFINITY;
+            }
             select(acc, sub0);
             maybe_compact();
         }
-        RT_PT(uint64_t c0 = clock64();)
         if (more) fetch_wait();
-        RT_PT(uint64_t c1 = clock64(); pc_wait += c1 - c0;)
         raw_barrier();
-        RT_PT(pc_bar += clock64() - c1;)
-        next_stage();
+        cur ^= 1;
     }
 
-    RT_PT(uint64_t c4 = clock64();)
     // ---- final selection, one query of the wave at a time ----
     __threadfence_block();
     float* os = a.out_s + static_cast<int64_t>(split) * nq * k;
@@ -512,7 +435,6 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
         const int64_t gq = qw + c;
         if (gq >= nq) break;
         Cand* b = cbase + static_cast<int64_t>(c) * kCap;
-        const int cnt = static_cast<int>((woff - woff0) / sizeof(Cand));
         int n0 = __shfl(cnt, c, 64), n1 = __shfl(cnt, c + 32, 64);
         if (n0 + n1 > 128) {
             float nt;
@@ -523,14 +445,6 @@ __global__ __launch_bounds__(512) void flatip_topk_v2_kernel(Args a, int splits,
         if (n0 + n1 <= 128) emit_sorted<2>(b, n0, n1, k, os + gq * k, oi + gq * k, a.id_offset);
         else emit_sorted<kE>(b, n0, n1, k, os + gq * k, oi + gq * k, a.id_offset);
     }
-#ifdef RT_TOPK_PROBE_TIMING
-    const uint64_t c5 = clock64();
-    const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesB + wave;
-    if (lane == 0 && gw < 65536) {
-        uint64_t* o = probe_cycles + gw * 6;
-        o[0] = c5 - pc_start; o[1] = pc_wait; o[2] = pc_bar; o[3] = pc_app; o[4] = pc_cmp; o[5] = c5 - c4;
-    }
-#endif
 }
 
 inline int planned_splits(int64_t q_tiles, int64_t nx) {

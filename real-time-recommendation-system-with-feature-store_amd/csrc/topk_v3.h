@@ -20,7 +20,6 @@
 // * three-stage LDS ring: tiles are DMA'd two stages ahead.
 #pragma once
 
-#include <type_traits>
 
 namespace rt {
 namespace topk {
@@ -35,7 +34,39 @@ using v2::kNT;
 using v2::kQT;
 using v2::kWavesB;
 using v2::lds_addr;
-using v2::wait_vm_le;
+
+// wait until at most n (wave-uniform, >= 0) vector-memory operations are in
+// flight — exactly n (capped at the counter's 63), so no candidate store's
+// acknowledgement is waited for
+template <int N>
+__device__ __forceinline__ void wait_vm_exact() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int LO, int HI>
+__device__ __forceinline__ void wait_vm_range(int n) {
+    if constexpr (LO == HI) {
+        wait_vm_exact<LO>();
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (n <= MID) wait_vm_range<LO, MID>(n);
+        else wait_vm_range<MID + 1, HI>(n);
+    }
+}
+__device__ __forceinline__ void wait_vm_le(int n) { wait_vm_range<0, 63>(n > 63 ? 63 : n); }
+
+#ifdef RT_TOPK_PROBE_TIMING
+// probe builds only (tools/hip_probe/topk_probe.hip): per-wave cycle attribution
+// [total, DMA wait, barrier, sub-tile steps, compaction, final]
+__device__ uint64_t probe_cycles[65536 * 6];
+inline void* probe_cycles_addr() {
+    void* p = nullptr;
+    (void)hipGetSymbolAddress(&p, HIP_SYMBOL(probe_cycles));
+    return p;
+}
+#define RT_PT(...) __VA_ARGS__
+#else
+#define RT_PT(...)
+#endif
 
 #ifndef RT_TOPK3_NT
 #define RT_TOPK3_NT 128
@@ -57,24 +88,28 @@ struct Cfg3 {
     static constexpr int TILE_BYTES = SLOTS * 16;
     static_assert(PIECES * 64 == SLOTS, "whole DMA pieces");
 };
-#ifndef RT_TOPK3_PREF_K
-#define RT_TOPK3_PREF_K 0
+#ifndef RT_TOPK3_PAIRCMP
+#define RT_TOPK3_PAIRCMP 0
 #endif
-constexpr int kPrefilterK = RT_TOPK3_PREF_K;
 #ifndef RT_TOPK3_LIMK
 #define RT_TOPK3_LIMK 2
 #endif
 constexpr int kRefreshMul = RT_TOPK3_LIMK;
+#ifndef RT_TOPK3_MAXK
+#define RT_TOPK3_MAXK 32
+#endif
+constexpr int kMaxKv3 = RT_TOPK3_MAXK;  // larger k runs v2 (see topk_impl.h)
 constexpr int kRing = RT_TOPK3_RING;  // LDS ring depth: 2 (DMA one stage ahead) or 3 (two)
 static_assert(kRing >= 2 && kRing <= 4, "ring of 2..4 stages");
 
-template <typename T, int S, bool EXCL, bool PREF>
+template <typename T, int S, bool EXCL>
 __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits, int64_t items_per_split) {
     using M = Mfma<T>;
     using C = Cfg3<T, S>;
     typedef typename M::frag frag;
     __shared__ __attribute__((aligned(1024))) char tile[kRing][C::TILE_BYTES];
     __shared__ __attribute__((aligned(16))) uint32_t hist[kWavesB][256];
+    __shared__ __attribute__((aligned(16))) float scr[kWavesB * 64 * 20];  // per-lane score rows (80 B: conflict-free b128)
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
     const char* __restrict__ Xb = reinterpret_cast<const char*>(a.X);
@@ -92,6 +127,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
     const int64_t q_pad = static_cast<int64_t>(gridDim.x / splits) * kQT;  // buffers per split
     Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32 buffers
     uint32_t* const whist = hist[wave];
+    float* const wscr = scr + (wave * 64 + lane) * 20;
 
     frag qf[S];
     {
@@ -111,7 +147,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
     const uint32_t* excl = (EXCL && qok) ? a.excl + q * a.excl_words : nullptr;
     float thr = qok ? -FLT_MAX : INFINITY;
 #ifdef RT_TOPK_PROBE_NOSEL
-    thr = INFINITY;  // probe builds only (tools/hip_probe/topk_probe.hip): the scan without selection
+    thr = INFINITY;  // probe builds only: the scan without selection
 #endif
 
     // append cursor (see v2): byte offset of the lane's next entry from the
@@ -123,9 +159,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
     const uint64_t wbase = (static_cast<uint64_t>(wb_hi) << 32) | wb_lo;
     const uint32_t woff0 = static_cast<uint32_t>((col * kCap + half * kHalf) * sizeof(Cand));
     uint32_t woff = woff0;
-    // checked once per stage: room for a whole stage's appends (16 rows per sub-tile);
+    // checked once per stage (or per pair of sub-tiles): room for the appends until the next check;
     // small k compacts early too — a half holding ~2k entries refreshes a stale threshold
-    const int lim_n = kRefreshMul > 0 ? min(kHalf - C::NSUB * 16, kRefreshMul * k + 32) : kHalf - C::NSUB * 16;
+    constexpr int kHead = RT_TOPK3_PAIRCMP ? 2 * 16 : C::NSUB * 16;  // appends between checks, at most
+    const int lim_n = kRefreshMul > 0 ? min(kHalf - kHead, kRefreshMul * k + 32) : kHalf - kHead;
     const uint32_t woff_lim = woff0 + static_cast<uint32_t>(lim_n * sizeof(Cand));
 
     // ---- DMA plan: this wave's pieces w, w+8, ... of a stage ----
@@ -183,35 +220,57 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         asm volatile("" ::: "memory");
     };
 
-    // ---- selection (same as v2: SGPR wave masks, masked dword-store appends) ----
-    auto appends = [&](const f32x16& acc, int64_t sub0, const uint64_t (&pm)[16], uint64_t any) {
-        if (!any) return;
-        const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
-        uint32_t xw = 0u;
-        if constexpr (EXCL) {
-            if (excl) xw = excl[sub0 >> 5];
-        }
+    // ---- selection ----
+    // Per lane (= per query, per half of the sub-tile's rows): a max-of-16
+    // filter against the query's threshold (most sub-tiles stop at the wave
+    // ballot); otherwise a 16-bit pass mask (2 VALU per score), the lane's scores
+    // staged in its LDS scratch row so the append loop can index them, and one
+    // append (two SADDR dword stores, the cursor advanced in place) per set bit,
+    // the wave looping max-over-lanes(popcount) times — 1 or 2 late in a scan.
+    auto max16 = [&](const f32x16& acc) {
+        float m = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            if (pm[r]) {
-                bool p;
-                if constexpr (EXCL) {
-                    p = acc[r] >= thr && !((xw >> tile_row(r, half)) & 1u);
-                    if (!__ballot(p)) continue;
-                } else {
-                    p = __builtin_amdgcn_inverse_ballot_w64(pm[r]);
-                }
-                issued += 2;
-                if (p) {
-                    // id = sub0 + tile_row(r, half): a per-sub-tile lane base + an immediate
-                    const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
-                    asm volatile(
-                        "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
-                        "v_add_u32 %0, 8, %0"
-                        : "+v"(woff)
-                        : "v"(acc[r]), "s"(wbase), "v"(id)
-                        : "memory");
-                }
+        for (int r = 3; r < 15; r += 2) m = fmaxf(fmaxf(m, acc[r]), acc[r + 1]);
+        return fmaxf(m, acc[15]);
+    };
+    auto appends = [&](const f32x16& acc, int64_t sub0, float m) {
+        if (__ballot(m >= thr) == 0) return;
+        uint32_t bits = 0u;  // bit 15-r <=> acc[r] passes
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            asm("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+                : "+v"(bits)
+                : "v"(acc[r]), "v"(thr)
+                : "vcc");
+        if constexpr (EXCL) {
+            if (excl) {
+                const uint32_t xw = excl[sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if ((xw >> tile_row(r, half)) & 1u) bits &= ~(1u << (15 - r));
+            }
+        }
+        if (bits) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<float4*>(wscr + 4 * i) =
+                    make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        }
+        const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
+        while (__ballot(bits != 0u)) {
+            issued += 2;  // exactly two store instructions for the wave
+            if (bits) {
+                const int b = 31 - __builtin_clz(bits);  // highest set bit = lowest r
+                bits &= ~(1u << b);
+                const int r = 15 - b;
+                const float v = wscr[r];  // same-wave LDS write → read: in order
+                const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
+                asm volatile(
+                    "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
+                    "v_add_u32 %0, 8, %0"
+                    : "+v"(woff)
+                    : "v"(v), "s"(wbase), "v"(id)
+                    : "memory");
             }
         }
     };
@@ -235,15 +294,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
 #pragma unroll
         for (int j = 0; j < kRing - 1; ++j) mk[j] = issued;  // drained
     };
-    auto select = [&](const f32x16& acc, int64_t sub0) {
-        uint64_t pm[16], any = 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            pm[r] = __ballot(acc[r] >= thr);
-            any |= pm[r];
-        }
-        appends(acc, sub0, pm, any);
-    };
+    auto select = [&](const f32x16& acc, int64_t sub0) { appends(acc, sub0, max16(acc)); };
 
     // ---- scan ----
     // A fragment (row block rt, k step s) of the stage in buffer cur: the lane
@@ -257,49 +308,26 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
     };
     // one sub-tile: acc = its scores; prev (the sub-tile before, item base subp)
     // compared in the MFMA gaps, then appended
+    // one sub-tile: acc = its scores; prev (the sub-tile before, item base subp)
+    // max-reduced in the MFMA gaps, then filtered / appended
     auto step = [&](const frag (&af)[S], f32x16& acc, const f32x16& prev, int64_t subp) {
-        uint64_t pm[16], any = 0;
         acc = f32x16{};
-        if constexpr (PREF) {
-            // small k: a max-of-16 (v_max3 tree) and one compare in the MFMA gaps;
-            // the per-row masks only when some lane of the wave passes
-            float m = 0.f;
+        float m = 0.f;
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                acc = M::run(af[s], qf[s], acc);
-                if (s == 0) m = fmaxf(fmaxf(prev[0], prev[1]), prev[2]);
-                if (s == 1) m = fmaxf(fmaxf(m, prev[3]), prev[4]);
-                if (s == 2) m = fmaxf(fmaxf(m, prev[5]), prev[6]);
-                if (s == 3) m = fmaxf(fmaxf(m, prev[7]), prev[8]);
-                if (s == 4 || (S < 8 && s == S - 1)) {
-                    m = fmaxf(fmaxf(m, prev[9]), prev[10]);
-                    m = fmaxf(fmaxf(m, prev[11]), prev[12]);
-                    m = fmaxf(fmaxf(m, prev[13]), prev[14]);
-                    m = fmaxf(m, prev[15]);
-                }
-            }
-            if (__ballot(m >= thr) == 0) return;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                pm[r] = __ballot(prev[r] >= thr);
-                any |= pm[r];
-            }
-        } else {
-            constexpr int CPG = (16 + S - 1) / S;
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                acc = M::run(af[s], qf[s], acc);
-#pragma unroll
-                for (int j = 0; j < CPG; ++j) {
-                    const int r = s * CPG + j;
-                    if (r < 16) {
-                        pm[r] = __ballot(prev[r] >= thr);
-                        any |= pm[r];
-                    }
-                }
+        for (int s = 0; s < S; ++s) {
+            acc = M::run(af[s], qf[s], acc);
+            if (s == 0) m = fmaxf(fmaxf(prev[0], prev[1]), prev[2]);
+            if (s == 1) m = fmaxf(fmaxf(m, prev[3]), prev[4]);
+            if (s == 2) m = fmaxf(fmaxf(m, prev[5]), prev[6]);
+            if (s == 3) m = fmaxf(fmaxf(m, prev[7]), prev[8]);
+            if (s == 4 || (S < 8 && s == S - 1)) {
+                m = fmaxf(fmaxf(m, prev[9]), prev[10]);
+                m = fmaxf(fmaxf(m, prev[11]), prev[12]);
+                m = fmaxf(fmaxf(m, prev[13]), prev[14]);
+                m = fmaxf(m, prev[15]);
             }
         }
-        appends(prev, subp, pm, any);
+        appends(prev, subp, m);
     };
     auto mask_tail = [&](f32x16& acc, int64_t sub0) {
         const int left = static_cast<int>(i_end - sub0);
@@ -337,13 +365,22 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         mk[kRing - 2] = issued;
         const char* stage = &tile[cur][0] + a_lane;
         RT_PT(const uint64_t c4s = clock64();)
+#if !RT_TOPK3_PAIRCMP
         maybe_compact();  // the only call site in the loop (keeps the call's register saves out of the steps)
+#endif
         RT_PT(const uint64_t c5s = clock64(); pc_cmp += c5s - c4s;)
         // sub-tiles in accumulators A, B, A, B, ... (the previous stage ended on B);
         // each sub-tile's A fragments are read while the one before computes
+#if RT_TOPK3_PAIRCMP
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
         for (int pr = 0; pr < C::NSUB / 2; ++pr) {
             const int r0 = 2 * pr, r1 = 2 * pr + 1;
+#if RT_TOPK3_PAIRCMP
+            maybe_compact();  // one call site: the pair loop is not unrolled
+#endif
             if (r0 * 32 < rem) {
                 step(af, accA, accB, subB);
                 if (r1 * 32 < rem) lds_a(af, stage, r1);
@@ -433,7 +470,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v3_kernel(Args a, int splits,
         const uint64_t c5 = clock64();
         const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesB + wave;
         if (lane == 0 && gw < 65536) {
-            uint64_t* o = v2::probe_cycles + gw * 6;
+            uint64_t* o = probe_cycles + gw * 6;
             o[0] = c5 - pc_start; o[1] = pc_wait; o[2] = pc_bar; o[3] = pc_steps; o[4] = pc_cmp; o[5] = c5 - c4;
         }
     }
@@ -444,22 +481,12 @@ template <typename T, int S>
 int launch_S(const Args& a, int splits, int64_t items_per_split, hipStream_t st) {
     const int64_t q_tiles = (a.nq + kQT - 1) / kQT;
     dim3 grid(static_cast<unsigned>(q_tiles * splits));
-    // small k: the max-of-16 prefilter (most sub-tiles pass no lane); large k:
-    // per-row compares straight away (nearly every sub-tile has a passing row)
-    const bool pref = a.k < kPrefilterK;
-    auto go = [&](auto ex, auto pf) {
-        hipLaunchKernelGGL((flatip_topk_v3_kernel<T, S, decltype(ex)::value, decltype(pf)::value>), grid,
-                           dim3(64 * kWavesB), 0, st, a, splits, items_per_split);
-    };
-    using TT = std::true_type;
-    using FF = std::false_type;
-    if (a.excl) {
-        if (pref) go(TT{}, TT{});
-        else go(TT{}, FF{});
-    } else {
-        if (pref) go(FF{}, TT{});
-        else go(FF{}, FF{});
-    }
+    if (a.excl)
+        hipLaunchKernelGGL((flatip_topk_v3_kernel<T, S, true>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                           items_per_split);
+    else
+        hipLaunchKernelGGL((flatip_topk_v3_kernel<T, S, false>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                           items_per_split);
     return check_launch("flatip_topk_v3_kernel");
 }
 
