@@ -311,33 +311,44 @@ def c1_epoch(dev):
                     "shape on the survey host, BASELINE.md §2)"}
 
 
-def _kernel_sources_sha() -> str:
+# the csrc files each PMC-profiled kernel family is built from (its traffic
+# figure is reused only while these are unchanged; tools/traffic_json.py)
+KERNEL_SOURCES = {
+    "linear_fwd": ["mlp.hip", "rt_common.h"], "linear_bwd_dz": ["mlp.hip", "rt_common.h"],
+    "linear_bwd_dw": ["mlp.hip", "rt_common.h"], "loss_fwd_bwd": ["loss.hip", "rt_common.h"],
+    "clip_adam": ["optim.hip", "rt_common.h"],
+    "flatip_topk_c4": ["topk_api.hip", "topk_f16.hip", "topk_impl.h", "topk_v1.h", "topk_v2.h", "topk_v3.h",
+                       "rt_sort.h", "rt_common.h"],
+}
+
+
+def _kernel_sources_sha(kernel: str) -> str:
     import hashlib
     h = hashlib.sha256()
     csrc = os.path.join(PKG, "csrc")
-    for f in sorted(os.listdir(csrc)):
-        if f.endswith((".hip", ".h")):
-            with open(os.path.join(csrc, f), "rb") as fh:
-                h.update(f.encode() + b"\0" + fh.read())
+    for f in sorted(KERNEL_SOURCES.get(kernel, [])):
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
     return h.hexdigest()[:16]
 
 
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of ``kernel`` from the newest profiles/*_traffic.json
-    whose kernel-source hash matches the sources being run (rocprofv3
-    FETCH_SIZE/WRITE_SIZE passes, tools/traffic_json.py); None if the PMC
-    profile is older than the kernels."""
+    whose hash of that kernel's sources matches the sources being run
+    (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, tools/traffic_json.py); None if the
+    PMC profile is older than the kernel."""
     import glob
-    sha = _kernel_sources_sha()
+    sha = _kernel_sources_sha(kernel)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), reverse=True):
         with open(path) as f:
             tj = json.load(f)
-        if tj.get("kernel_sources_sha") != sha:
+        shas = tj.get("kernel_sources_sha")
+        if not isinstance(shas, dict) or shas.get(kernel) != sha:
             continue
         tb = tj.get("bytes_per_launch", {}).get(kernel)
         if tb is not None:
             return float(tb), f"{os.path.relpath(path, REPO)}: " + tj.get("correction", "")
-    return None, f"no PMC profile of these kernel sources (sha {sha}) under profiles/"
+    return None, f"no PMC profile of these {kernel} sources (sha {sha}) under profiles/"
 
 
 def topk_c4_scaling(dev, dist, rank, world, reps=3):

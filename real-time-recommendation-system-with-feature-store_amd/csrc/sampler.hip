@@ -13,6 +13,7 @@
 // a lower lane's same-round proposal, and retries until every slot holds a value.
 // Distinctness is exact; the accepted set is uniform over the pool because each
 // round's proposals are uniform and rejection only removes forbidden values.
+// Catalogues up to 65,536 items test membership in a per-wave LDS bitmap.
 #include "rt_common.h"
 
 namespace rt {
@@ -37,6 +38,14 @@ __device__ __forceinline__ bool contains(const int32_t* __restrict__ items, int6
     return a < hi && items[a] == c;
 }
 
+// BITMAP: the catalogue fits a per-wave LDS bitmap (num_items <= kMaxBitmapItems):
+// the user's positives are set in it once, accepted negatives are added as
+// they are taken, so every membership test is one LDS read instead of a
+// dependent binary search through global memory. Same draws, same acceptance
+// rule, same output as the search form.
+constexpr int64_t kMaxBitmapItems = 65536;
+
+template <bool BITMAP>
 __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __restrict__ offsets,
                                                                const int32_t* __restrict__ items, int64_t n_users,
                                                                const int64_t* __restrict__ users, int64_t n,
@@ -45,6 +54,7 @@ __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __
                                                                int64_t* __restrict__ out) {
     __shared__ int32_t acc_s[4][kMaxNeg];
     __shared__ int32_t prop_s[4][kMaxNeg];
+    extern __shared__ uint32_t bits_s[];  // BITMAP: [4][words]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + w;
     if (row >= n) return;
@@ -54,12 +64,27 @@ __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __
     if (u >= 0 && u < n_users) { lo = offsets[u]; hi = offsets[u + 1]; }
     const int64_t pool = num_items - (hi - lo);
     int64_t* o = out + row * num_neg;
+    const int words = static_cast<int>((num_items + 31) / 32);
+    uint32_t* const bits = bits_s + static_cast<int64_t>(w) * words;
+    if constexpr (BITMAP) {
+        for (int i = lane; i < words; i += 64) bits[i] = 0u;
+        wave_lds_sync();
+        for (int64_t i = lo + lane; i < hi; i += 64) {
+            const int32_t it = items[i];
+            if (it >= 0 && it < num_items) atomicOr(&bits[it >> 5], 1u << (it & 31));
+        }
+        wave_lds_sync();
+    }
+    auto forbidden = [&](int32_t c) -> bool {
+        if constexpr (BITMAP) return (bits[c >> 5] >> (c & 31)) & 1u;
+        else return contains(items, lo, hi, c);
+    };
     if (pool <= num_neg) {
         // the whole pool in id order (reference: `return negative_pool`), -1 padded
         int written = 0;
         for (int64_t base = 0; base < num_items && written < num_neg; base += 64) {
             const int64_t c = base + lane;
-            const bool keep = c < num_items && !contains(items, lo, hi, static_cast<int32_t>(c));
+            const bool keep = c < num_items && !forbidden(static_cast<int32_t>(c));
             const uint64_t m = __ballot(keep);
             const int before = __popcll(m & ((1ull << lane) - 1ull));
             if (keep && written + before < num_neg) o[written + before] = c;
@@ -81,16 +106,17 @@ __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __
         }
         if (lane < kMaxNeg) prop_s[w][lane] = c;
         wave_lds_sync();
-        bool ok = want && !contains(items, lo, hi, c);
+        bool ok = want && !forbidden(c);  // BITMAP: the accepted negatives are in the bitmap too
         if (ok) {
-            for (int j = 0; j < num_neg; ++j) {
-                if (acc_s[w][j] == c || (j < lane && prop_s[w][j] == c)) { ok = false; break; }
+            for (int j = 0; j < (BITMAP ? lane : num_neg); ++j) {
+                if ((!BITMAP && acc_s[w][j] == c) || (j < lane && prop_s[w][j] == c)) { ok = false; break; }
             }
         }
         wave_lds_sync();
         if (ok) {
             mine = c;
-            acc_s[w][lane] = c;
+            if constexpr (BITMAP) atomicOr(&bits[c >> 5], 1u << (c & 31));
+            else acc_s[w][lane] = c;
         }
         wave_lds_sync();
     }
@@ -110,7 +136,13 @@ extern "C" int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* po
     if (n == 0) return RT_OK;
     if (!pos_offsets || !users || !out || (!pos_items && n_users > 0)) return RT_ERR_INVALID;
     const dim3 grid(static_cast<unsigned>((n + 3) / 4));
-    hipLaunchKernelGGL(sampler::sample_negatives_kernel, grid, dim3(256), 0, as_stream(stream), pos_offsets,
-                       pos_items, n_users, users, n, num_items, num_neg, seed, seed_offset, out);
+    if (num_items <= sampler::kMaxBitmapItems) {
+        const size_t lds = 4 * static_cast<size_t>((num_items + 31) / 32) * sizeof(uint32_t);
+        hipLaunchKernelGGL(sampler::sample_negatives_kernel<true>, grid, dim3(256), lds, as_stream(stream),
+                           pos_offsets, pos_items, n_users, users, n, num_items, num_neg, seed, seed_offset, out);
+    } else {
+        hipLaunchKernelGGL(sampler::sample_negatives_kernel<false>, grid, dim3(256), 0, as_stream(stream),
+                           pos_offsets, pos_items, n_users, users, n, num_items, num_neg, seed, seed_offset, out);
+    }
     return check_launch("sample_negatives_kernel");
 }

@@ -54,6 +54,28 @@ def test_sampler_contract(device):
         assert not set(row.tolist()) & pos
 
 
+def test_sampler_contract_large_catalogue(device):
+    """Catalogues over 65,536 items take the binary-search form (no LDS bitmap):
+    same contract."""
+    rng = np.random.default_rng(5)
+    n_users, num_items, num_neg = 16, 100_000, 16
+    users_l, items_l = [], []
+    for u in range(n_users):
+        its = rng.choice(num_items, int(rng.integers(1, 3000)), replace=False)
+        users_l.append(np.full(len(its), u))
+        items_l.append(its)
+    csr = PositiveCSR.from_pairs(np.concatenate(users_l), np.concatenate(items_l), n_users)
+    dcsr = csr.to(device)
+    users = torch.from_numpy(rng.integers(0, n_users, 2000)).to(device)
+    o = kernels.sample_negatives(dcsr.offsets, dcsr.items, users, num_items, num_neg, seed=11).cpu().numpy()
+    for r, u in enumerate(users.cpu().numpy()):
+        row = o[r]
+        pos = set(csr.items[csr.offsets[u]:csr.offsets[u + 1]].tolist())
+        assert len(set(row.tolist())) == num_neg
+        assert ((row >= 0) & (row < num_items)).all()
+        assert not set(row.tolist()) & pos
+
+
 def test_sampler_is_uniform_over_the_pool(device):
     rng = np.random.default_rng(1)
     num_items, num_neg = 200, 8

@@ -16,14 +16,15 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     "real-time-recommendation-system-with-feature-store_amd", "csrc")
 
 
-def kernel_sources_sha() -> str:
-    """Same hash as bench.py::_kernel_sources_sha (which refuses a stale profile)."""
-    h = hashlib.sha256()
-    for f in sorted(os.listdir(CSRC)):
-        if f.endswith((".hip", ".h")):
-            with open(os.path.join(CSRC, f), "rb") as fh:
-                h.update(f.encode() + b"\0" + fh.read())
-    return h.hexdigest()[:16]
+def _bench_module():
+    """bench.py's KERNEL_SOURCES / _kernel_sources_sha (one definition of the hash)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_for_sha", os.path.join(os.path.dirname(CSRC), "..",
+                                                                                "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
 
 FAMILY = {"linear_fwd_kernel": ["linear_fwd"], "linear_bwd_dz_kernel": ["linear_bwd_dz"],
           "linear_bwd_dw_kernel": ["linear_bwd_dw"], "loss_fwd_kernel": ["loss_fwd_bwd"],
@@ -61,6 +62,6 @@ for (name, fam), b in tot.items():
 json.dump({"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes: "
                      "bench.py --steps 10 --warmup 3 --no-extras --no-cpu-baseline and tools/prof_topk.py 100 2",
            "correction": "bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halves wide 16-B/lane reads)",
-           "kernel_sources_sha": kernel_sources_sha(),
+           "kernel_sources_sha": {k: _bench_module()._kernel_sources_sha(k) for k in per},
            "bytes_per_launch": {k: round(v) for k, v in per.items()}}, sys.stdout, indent=1)
 print()
