@@ -399,6 +399,46 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
             "scaling": "strong (fixed 1M-row corpus)"}
 
 
+def topk_c4_replicated(dev, dist, rank, world, reps=3):
+    """C4 alternative layout, run collectively: the 1M-row f16 corpus (256 MB)
+    REPLICATED on every GPU and the 65,536 queries of a launch split over the
+    ranks (shard_range) — no exchange, no merge, each rank's lists final.
+    Strong scaling on the same workload as topk_c4_1m_sharded; the row-sharded
+    form keeps per-(query, shard) selection work that does not shrink with N."""
+    from rtrec_amd import kernels
+    from rtrec_amd.dist.sharded import shard_range
+    n, d, nq, k = 1_000_000, 128, 65536, 100
+    g = torch.Generator(device=dev).manual_seed(4242)  # same corpus on every rank
+    corpus = torch.nn.functional.normalize(torch.randn(n, d, device=dev, generator=g), dim=1).half()
+    gq = torch.Generator(device=dev).manual_seed(99)
+    q = torch.nn.functional.normalize(torch.randn(nq, d, device=dev, generator=gq), dim=1).half()
+    qb, qc = shard_range(nq, world, rank)
+    mine = q[qb:qb + qc].contiguous()
+
+    def sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    kernels.flatip_topk(mine, corpus, k)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        kernels.flatip_topk(mine, corpus, k)
+    sync()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    del corpus, q, mine
+    torch.cuda.empty_cache()
+    return {"qps": nq * reps / el, "ms_per_launch": 1e3 * el / reps, "n_gpus": world, "corpus_rows": n,
+            "queries_per_rank": qc, "k": k, "dtype": "f16", "exchange": "none (corpus replicated, queries split)",
+            "scaling": "strong (fixed 1M-row corpus, 65,536 queries per launch)"}
+
+
 def c5_sharded_step(dev, dist, rank, world, reps=10):
     """C5 leg (SURVEY §8(e) training row), run collectively on every rank: a
     100M-row x 256 bf16 item table row-sharded 12.5M rows (6.4 GB) per GPU
@@ -578,7 +618,7 @@ def main():
                    "parallelism": f"dp{world}", "final_loss": final_loss},
         "roofline": roof,
     }
-    scaling = c5 = None
+    scaling = c5 = repl = None
     if not args.no_extras:  # collective: every rank
         try:
             scaling = topk_c4_scaling(dev, dist, rank, world)
@@ -588,6 +628,10 @@ def main():
             c5 = c5_sharded_step(dev, dist, rank, world)
         except Exception as e:
             c5 = {"error": repr(e)}
+        try:
+            repl = topk_c4_replicated(dev, dist, rank, world)
+        except Exception as e:
+            repl = {"error": repr(e)}
     if rank == 0 and world == 1:
         if not args.no_extras:
             try:
@@ -610,6 +654,8 @@ def main():
                 result["cpu_baseline"]["topk"] = {"error": repr(e)}
     if c5 is not None:
         result.setdefault("extras", {})["c5_sharded_step"] = c5
+    if repl is not None:
+        result.setdefault("extras", {})["topk_c4_1m_replicated"] = repl
     if scaling is not None:
         result.setdefault("extras", {})["topk_c4_1m_sharded"] = scaling
         cb = result.get("cpu_baseline", {}).get("topk", {}).get("topk_c4")
