@@ -16,7 +16,9 @@
   all-gathered and a permutation gather puts every row in batch order on every
   rank (copies only).
 * Data-parallel in-batch step of config C5 (:func:`sharded_inbatch_step`):
-  each rank scores its own users against the whole gathered batch of items.
+  each rank scores its own users against the whole gathered batch of items;
+  for a trainable table the item-row gradients go back to their owners with
+  one reduce-scatter (:func:`sharded_scatter_add_rows`).
 * Data-parallel training: the flat fp32 grad slab is averaged with one
   all-reduce (see training/fused_step.py).
 
@@ -173,6 +175,57 @@ def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Te
     slot = torch.empty_like(owner)
     slot[order] = torch.arange(owner.numel(), device=dev) - starts[owner[order]]
     return gather(segs, owner * seg + slot, 0)
+
+
+def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_ids: torch.Tensor,
+                             grad_rows: torch.Tensor, group=None,
+                             scatter_add: Optional[Callable] = None) -> torch.Tensor:
+    """Backward of :func:`sharded_gather_rows` for a TRAINABLE row-sharded table
+    (the nn.Embedding path a2 under C5 sharding, SURVEY §8(e) "next"): every rank
+    holds its d loss / d rows for the whole global batch (``grad_rows`` [B_total,
+    D], rows in the order of ``global_ids``); the owner of each row receives the
+    sum over ranks and adds it into its shard's gradient (``grad_shard`` [rows,
+    D], shard rows start at global ``row_begin``).
+
+    One reduce-scatter moves each row's gradient once per rank: positions are
+    ordered by owner (stable), each owner's segment padded to the largest
+    segment, summed over ranks by ``reduce_scatter_tensor`` (an all-reduce of the
+    same buffer on gloo, which has no reduce-scatter), and the owner's segment is
+    scatter-added (``rt_scatter_add_rows_f32``; repeated ids accumulate)."""
+    scatter_add = scatter_add or (lambda t, ids, g: kernels.scatter_add_rows(t, ids, g))
+    world, rank = _world(group)
+    ids = global_ids.to(torch.int64)
+    if world == 1:
+        return scatter_add(grad_shard, ids - row_begin, grad_rows)
+    dev = ids.device
+    win = torch.tensor([int(row_begin), int(row_begin) + grad_shard.shape[0]], dtype=torch.int64, device=dev)
+    all_win = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(all_win, win, group=group)
+    all_win = all_win.view(world, 2)
+    owner = torch.searchsorted(all_win[:, 0].contiguous(), ids, right=True) - 1
+    if bool(((owner < 0) | (ids >= all_win[owner.clamp(min=0), 1])).any()):
+        raise IndexError("batch id outside every rank's table window")
+    per_owner = torch.bincount(owner, minlength=world)
+    seg = int(per_owner.max())
+    if seg == 0:
+        return grad_shard
+    order = torch.argsort(owner, stable=True)
+    starts = torch.cumsum(per_owner, 0) - per_owner
+    slot = torch.arange(ids.numel(), device=dev) - starts[owner[order]]
+    d = grad_rows.shape[1]
+    send = torch.zeros((world * seg, d), dtype=grad_rows.dtype, device=grad_rows.device)
+    send[owner[order] * seg + slot] = grad_rows[order]
+    recv = torch.empty((seg, d), dtype=grad_rows.dtype, device=grad_rows.device)
+    if dist.get_backend(group) == "gloo":
+        dist.all_reduce(send, op=dist.ReduceOp.SUM, group=group)
+        recv.copy_(send[rank * seg:(rank + 1) * seg])
+    else:
+        dist.reduce_scatter_tensor(recv, send, op=dist.ReduceOp.SUM, group=group)
+    n_mine = int(per_owner[rank])
+    if n_mine:
+        mine_ids = ids[order[starts[rank]:starts[rank] + n_mine]]
+        scatter_add(grad_shard, mine_ids - row_begin, recv[:n_mine])
+    return grad_shard
 
 
 def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: torch.Tensor,

@@ -20,6 +20,7 @@ import torch.multiprocessing as mp
 
 from oracle import flat_ip as orc
 from rtrec_amd.dist.sharded import (allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_inbatch_step,
+                                    sharded_scatter_add_rows,
                                sharded_topk, sharded_topk_owner)
 
 
@@ -155,6 +156,33 @@ def test_sharded_gather_rows_gloo(world, counts, skew):
     skewed onto one owner (empty segments elsewhere): rows in batch order,
     bit-exact."""
     _run(world, _gather_worker, 997, 16, 3, counts, skew)
+
+
+def _scatter_worker(rank, world, n, d, b, seed):
+    rng = np.random.default_rng(seed)
+    ids = rng.integers(0, n, size=b)
+    ids[: b // 4] = ids[0]                       # repeated ids accumulate
+    grads = [rng.standard_normal((b, d)).astype(np.float32) for _ in range(world)]  # every rank's contribution
+    ref = np.zeros((n, d), np.float64)
+    for g in grads:
+        np.add.at(ref, ids, g)
+    rb, rc = shard_range(n, world, rank)
+    shard_grad = torch.zeros((rc, d))
+
+    def scatter_add(t, loc, g):  # rt_scatter_add_rows_f32 semantics on CPU
+        t.index_add_(0, loc, g)
+        return t
+
+    sharded_scatter_add_rows(shard_grad, rb, torch.from_numpy(ids), torch.from_numpy(grads[rank]),
+                             scatter_add=scatter_add)
+    np.testing.assert_allclose(shard_grad.numpy(), ref[rb:rb + rc], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_scatter_add_rows_gloo(world):
+    """Trainable C5 table: row gradients of the global batch summed over ranks
+    and added into their owners' shards (one reduce-scatter by owner segment)."""
+    _run(world, _scatter_worker, 301, 8, 64, 13)
 
 
 def _dp_worker(rank, world):

@@ -97,6 +97,50 @@ def main():
             print(f"bwd m={m:5d} k={k:3d} n={n:3d} {label:14s} {us:8.1f} {fl / us / 1e6:7.2f}")
 
 
+def fwd_epilogues():
+    """The C2 step's forward shapes (m = 18,432, BN-train + dropout prologue,
+    two BN segments) with each epilogue: raw z, z + next-BN stats, and the
+    final layer's row L2 normalisation."""
+    dev = torch.device("cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    S = 16
+    m, seg = 18432, 1024
+    for (k, n) in [(256, 128), (128, 128)]:
+        src = torch.randn(m, k, device=dev)
+        w = torch.randn(n, k, device=dev) * 0.05
+        b = torch.zeros(n, device=dev)
+        z = torch.empty(m, n, device=dev)
+        out = torch.empty(m, n, device=dev)
+        norms = torch.empty(m, device=dev)
+        stats_prev = torch.zeros(2 * S * 2 * k, dtype=torch.float64, device=dev)
+        stats_prev.view(2, S, 2, k)[:, 0, 0] = 0.1 * m
+        stats_prev.view(2, S, 2, k)[:, 0, 1] = 1.0 * m
+        gam, bet = torch.ones(k, device=dev), torch.zeros(k, device=dev)
+        rm, rv = torch.zeros(k, device=dev), torch.ones(k, device=dev)
+        sm, si = torch.empty(2 * k, device=dev), torch.empty(2 * k, device=dev)
+        stats = torch.zeros(2 * S * 2 * n, dtype=torch.float64, device=dev)
+        for label in ("z", "z+stats", "l2norm", "two-seg z+stats", "two-seg l2norm"):
+            a = LinearFwdArgs()
+            a.src, a.src_rows, a.ld_src, a.m, a.k, a.n = src.data_ptr(), m, k, m, k, n
+            a.w, a.bias, a.act = w.data_ptr(), b.data_ptr(), 0
+            a.prev_mode, a.prev_act = 1, 0
+            a.prev_stats, a.bn_gamma, a.bn_beta = stats_prev.data_ptr(), gam.data_ptr(), bet.data_ptr()
+            a.running_mean, a.running_var = rm.data_ptr(), rv.data_ptr()
+            a.save_mean, a.save_invstd = sm.data_ptr(), si.data_ptr()
+            a.bn_eps, a.bn_momentum = 1e-5, 0.1
+            a.drop_p, a.drop_seed = 0.2, 7
+            if label.startswith("two-seg"):
+                a.seg_split = seg
+            if label.endswith("l2norm"):
+                a.l2_out, a.norms_out = out.data_ptr(), norms.data_ptr()
+            else:
+                a.z_out = z.data_ptr()
+                if "stats" in label:
+                    a.stats_out = stats.data_ptr()
+            us = timeit(lambda: call("rt_linear_fwd_f32", ctypes.byref(a), st))
+            print(f"fwd m={m} k={k:3d} n={n:3d} {label:18s} {us:8.1f} us {2 * m * k * n / us / 1e6:7.2f} TF/s")
+
+
 def split_bwd():
     """dz and dW launches timed separately at the C2 item-tower shapes (17,408
     rows), hidden-layer form, with and without the dropout prologue."""
@@ -143,5 +187,8 @@ if __name__ == "__main__":
     if "--split" in sys.argv:
         native.lib()
         split_bwd()
+    elif "--fwd-epi" in sys.argv:
+        native.lib()
+        fwd_epilogues()
     else:
         main()
