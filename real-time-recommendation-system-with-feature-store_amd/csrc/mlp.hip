@@ -324,6 +324,55 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
 
     // ---- epilogue ----
     const bool l2 = a.l2_out != nullptr;
+    // final layer, fast form: z² staged column-major in the (now idle) A tile,
+    // row sums by 8 threads per row (DPP butterfly), one sqrt and one division
+    // per row, then a multiply per element — instead of a 32-lane shuffle
+    // reduction per row and a division per element
+    if (l2 && !a.z_out && !a.stats_out && n * (FM + 1) <= FM * lda) {
+        __syncthreads();  // every wave is done reading As
+        float* zsq = As;  // [n][FM + 1]
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int col = (w + 4 * i) * 32 + c32;
+            if ((w + 4 * i) * 32 >= n) continue;  // wave-uniform
+            const bool col_ok = col < n;
+            const float b = (col_ok && a.bias) ? a.bias[col] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const float z = acc[i][r] + b;
+                acc[i][r] = z;
+                if (col_ok) zsq[col * (FM + 1) + lr] = (row0 + lr < m) ? z * z : 0.f;
+            }
+        }
+        __syncthreads();
+        {
+            const int row = tid >> 3, part = tid & 7;  // 32 rows x 8 threads
+            float ss = 0.f;
+            for (int c = part; c < n; c += 8) ss += zsq[c * (FM + 1) + row];
+            ss += __shfl_xor(ss, 1, 64);
+            ss += __shfl_xor(ss, 2, 64);
+            ss += __shfl_xor(ss, 4, 64);
+            if (part == 0) {
+                const float nrm = sqrtf(ss);
+                rowpart[row] = 1.f / fmaxf(nrm, kNormEps);
+                if (row0 + row < m && a.norms_out) a.norms_out[row0 + row] = nrm;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int col = (w + 4 * i) * 32 + c32;
+            if ((w + 4 * i) * 32 >= n) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const int64_t gr = row0 + lr;
+                if (gr < m && col < n) a.l2_out[gr * n + col] = acc[i][r] * rowpart[lr];
+            }
+        }
+        return;
+    }
     double* const stats = a.stats_out ? a.stats_out + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
                                                        bid % RT_STAT_SLOTS) * 2 * n : nullptr;
 #pragma unroll
