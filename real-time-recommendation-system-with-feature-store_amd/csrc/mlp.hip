@@ -123,6 +123,27 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
     if (blockIdx.x == 0 && a.zero_buf)
         for (int64_t e = tid; e < a.zero_words; e += 256) a.zero_buf[e] = 0.0;
 
+    // A-tile fast path (float4 rows, piecewise-linear act): without a row gather
+    // the tile's loads are issued HERE, before the BatchNorm finalisation below,
+    // so its fp64 slot reads and the tile reads share one memory round trip
+    const int vpr = kp / 4;
+    const bool vec = (a.ld_src % 4) == 0 && (reinterpret_cast<uintptr_t>(a.src) & 15) == 0;
+    const bool fast = vec && (a.k % 4) == 0 && (256 % vpr) == 0 &&
+                      (a.prev_mode == 0 || act_is_piecewise_linear(a.prev_act));
+    const bool early = fast && !a.ids && 8 * (256 / vpr) >= FM;  // one pass covers the tile
+    float4 pre[8];
+    if (early) {
+        const int c = (tid % vpr) * 4, rstep = 256 / vpr, r0 = tid / vpr;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int r = r0 + u * rstep;
+            const int64_t gr = row0 + r;
+            pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (r < FM && c < k && gr < m && gr < a.src_rows)
+                pre[u] = *reinterpret_cast<const float4*>(a.src + gr * a.ld_src + c);
+        }
+    }
+
     // BatchNorm of the previous block: this block's batch is its row segment;
     // block 0 derives every segment (it owns the save/running-stat writes,
     // applied in segment order like two sequential tower calls)
@@ -177,10 +198,8 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
     const Pro pro{a.prev_mode, a.prev_act, a.drop_p, a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f, seed,
                   scale, shift};
     {   // stage the transformed A tile: float4 loads, 4 in flight per thread
-        const int vpr = kp / 4;
         const int total = FM * vpr;
-        const bool vec = (a.ld_src % 4) == 0 && (reinterpret_cast<uintptr_t>(a.src) & 15) == 0;
-        if (vec && (a.k % 4) == 0 && (256 % vpr) == 0 && (pro.mode == 0 || act_is_piecewise_linear(pro.act))) {
+        if (fast) {
             // fast path: 4 fixed columns per thread (BN affine in registers, no
             // per-element division / LDS reads / act switch), rows strided by 256/vpr
             const int c = (tid % vpr) * 4, rstep = 256 / vpr;
@@ -195,7 +214,9 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
                 for (int u = 0; u < 8; ++u) {
                     const int r = r0 + u * rstep;
                     v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (r < FM && c < k) {
+                    if (early) {
+                        v[u] = pre[u];
+                    } else if (r < FM && c < k) {
                         const int64_t sr = srow[r];
                         if (sr >= 0) v[u] = *reinterpret_cast<const float4*>(a.src + sr * a.ld_src + c);
                     }
@@ -454,8 +475,10 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
 // ---------------------------------------------------------------------------
 // Block = 32 rows. dz (32 x n) lives in LDS; dA = dz·W reads W[n][k] rows
 // coalesced along k straight from L2 (the reduction runs over n).
+// (3 waves per SIMD: the C2 launches' 576 blocks need 3 co-resident blocks on
+// some CUs; the register cap moves the accumulators from AGPRs to VGPRs, no spill)
 template <int TPWK>  // 32-col dA tiles per wave (k <= 128*TPWK)
-__global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void linear_bwd_dz_kernel(BwdLaunch L) {
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
@@ -542,6 +565,24 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
         float* cI = cM + np;         // invstd
         const float inv_m = 1.f / static_cast<float>(seg_m);
         const double* gst = a.g_stats ? a.g_stats + static_cast<int64_t>(my_seg) * RT_STAT_SLOTS * 2 * n : nullptr;
+        const int vpr = np / 4;
+        const bool vec = (n % 4) == 0;
+        const bool fast = vec && (256 % vpr) == 0 && act_is_piecewise_linear(a.act) && a.grad_mode != 3;
+        // fast path with one pass over the tile: its g loads are issued before
+        // the coefficient loads below, so both share one memory round trip (z
+        // follows after the barrier: both sets at once would cost occupancy)
+        const bool early = fast && 8 * (256 / vpr) >= FM;
+        float4 pg[8];
+        if (early) {
+            const int c = (tid % vpr) * 4, rstep = 256 / vpr, r0 = tid / vpr;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int r = r0 + u * rstep;
+                const int64_t gr = row0 + r;
+                pg[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (r < FM && gr < m && c < n) pg[u] = *reinterpret_cast<const float4*>(a.g + gr * n + c);
+            }
+        }
         for (int c = tid; c < np; c += 256) {
             float A = 1.f, Bc = 0.f, C = 0.f, M = 0.f, I = 1.f;
             if (c < n && (a.grad_mode == 1 || a.grad_mode == 2)) {
@@ -558,10 +599,8 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
             cA[c] = A; cB[c] = Bc; cC[c] = C; cM[c] = M; cI[c] = I;
         }
         __syncthreads();
-        const int vpr = np / 4;
         const int total = FM * vpr;
-        const bool vec = (n % 4) == 0;
-        if (vec && (256 % vpr) == 0 && act_is_piecewise_linear(a.act) && a.grad_mode != 3) {
+        if (fast) {
             // fast path: each thread owns 4 fixed columns (coefficients in
             // registers, no per-element division or LDS reads), rows strided by
             // 256/vpr; all g/z loads of the thread issued before the math
@@ -578,7 +617,10 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
                     const int64_t gr = row0 + r;
                     gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
                     zv[u] = gv[u];
-                    if (r < FM && gr < m && c < n) {
+                    if (early) {
+                        gv[u] = pg[u];
+                        if (r < FM && gr < m && c < n) zv[u] = *reinterpret_cast<const float4*>(a.z + gr * n + c);
+                    } else if (r < FM && gr < m && c < n) {
                         gv[u] = *reinterpret_cast<const float4*>(a.g + gr * n + c);
                         zv[u] = *reinterpret_cast<const float4*>(a.z + gr * n + c);
                     }
@@ -694,6 +736,23 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
     // (the W pointer read once: inside the conditional loads below a field of
     // the selected launch group was re-loaded from the kernarg segment per load)
     const float* __restrict__ Wt = a.w;
+    const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
+    // fast epilogue (the C2 hidden layers): a full row block, g_prev only, a
+    // piecewise-linear previous activation — no per-element predicates, 32-bit
+    // offsets from one base pointer; its z_prev / BN loads are issued HERE,
+    // ahead of the reduction, so they land during the MFMAs
+    const bool fast = row0 + FM <= m && !a.dsrc && a.g_prev && act_is_piecewise_linear(a.prev_act);
+    float zpre[TPWK][16], pmean[TPWK], pinv[TPWK];
+#pragma unroll
+    for (int i = 0; i < TPWK; ++i) {
+        const int kk = (w + 4 * i) * 32 + c32;
+        const bool ld = fast && want_stats && kk < k;
+        pmean[i] = ld ? a.prev_mean[my_seg * k + kk] : 0.f;
+        pinv[i] = ld ? a.prev_invstd[my_seg * k + kk] : 0.f;
+        const float* zp = a.src + (row0 + 4 * h) * a.ld_src + kk;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) zpre[i][r] = ld ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
+    }
     auto load_w = [&](int s, float (&dst)[TPWK][8]) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
@@ -731,29 +790,20 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
     }
     const float pscale = a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f;
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
-    const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
     double* const gps = want_stats ? a.g_prev_stats + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
                                                         bid % RT_STAT_SLOTS) * 2 * k : nullptr;
-    // fast epilogue (the C2 hidden layers): a full row block, g_prev only, a
-    // piecewise-linear previous activation — no per-element predicates, 32-bit
-    // offsets from one base pointer, every z_prev load issued before the math
-    const bool fast = row0 + FM <= m && !a.dsrc && a.g_prev && act_is_piecewise_linear(a.prev_act);
     const float psl = act_slope(a.prev_act);
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
         const int kk = (w + 4 * i) * 32 + c32;
         const bool col_ok = kk < k;
         float s1 = 0.f, s2 = 0.f;
-        float pmean = 0.f, pinv = 0.f;
-        if (want_stats && col_ok) { pmean = a.prev_mean[my_seg * k + kk]; pinv = a.prev_invstd[my_seg * k + kk]; }
         if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform: tile past k
         if (fast) {
             const int64_t rb = row0 + 4 * h;
-            const float* zp = a.src + rb * a.ld_src + kk;
             float* gp = a.g_prev + rb * k + kk;
-            float zv[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) zv[r] = (want_stats && col_ok) ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
+            const float* zv = zpre[i];
+            const float pm = pmean[i], pi = pinv[i];
             const bool drop = a.prev_drop_p > 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
@@ -761,7 +811,7 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
                 float gv = acc[i][r];
                 if (drop) gv = dropout_keep(pseed, rb + lr, kk, a.prev_drop_p) ? gv * pscale : 0.f;
                 if (col_ok) gp[lr * k] = gv;
-                const float xh = (act_pwl(psl, zv[r]) - pmean) * pinv;
+                const float xh = (act_pwl(psl, zv[r]) - pm) * pi;
                 s1 += gv;
                 s2 += gv * xh;
             }
@@ -779,7 +829,8 @@ __global__ __launch_bounds__(256) void linear_bwd_dz_kernel(BwdLaunch L) {
                         gv = dropout_keep(pseed, gr, kk, a.prev_drop_p) ? da * pscale : 0.f;
                     a.g_prev[gr * k + kk] = gv;
                     if (want_stats) {
-                        const float xh = (act_eval(a.prev_act, a.src[gr * a.ld_src + kk]) - pmean) * pinv;
+                        const float xh = (act_eval(a.prev_act, a.src[gr * a.ld_src + kk]) -
+                                          a.prev_mean[my_seg * k + kk]) * a.prev_invstd[my_seg * k + kk];
                         s1 += gv;
                         s2 += gv * xh;
                     }

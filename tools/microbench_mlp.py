@@ -141,6 +141,48 @@ def fwd_epilogues():
             print(f"fwd m={m} k={k:3d} n={n:3d} {label:18s} {us:8.1f} us {2 * m * k * n / us / 1e6:7.2f} TF/s")
 
 
+def fwd_attr():
+    """Attribution of the hidden-layer forward (k = 256 -> n = 128): prologue
+    mode x epilogue x row count, so the fixed per-launch cost, the BN/dropout
+    prologue and the stats epilogue separate."""
+    dev = torch.device("cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    S = 16
+    k, n = 256, 128
+    tiny = torch.zeros(64, device=dev)
+    print(f"launch floor (64-element fill) {timeit(lambda: tiny.zero_()):8.1f} us")
+    for m in (8192, 16384, 18432, 24576):
+        src = torch.randn(m, k, device=dev)
+        w = torch.randn(n, k, device=dev) * 0.05
+        b = torch.zeros(n, device=dev)
+        z = torch.empty(m, n, device=dev)
+        stats_prev = torch.zeros(2 * S * 2 * k, dtype=torch.float64, device=dev)
+        stats_prev.view(2, S, 2, k)[:, 0, 0] = 0.1 * m
+        stats_prev.view(2, S, 2, k)[:, 0, 1] = 1.0 * m
+        gam, bet = torch.ones(k, device=dev), torch.zeros(k, device=dev)
+        rm, rv = torch.zeros(k, device=dev), torch.ones(k, device=dev)
+        sm, si = torch.empty(2 * k, device=dev), torch.empty(2 * k, device=dev)
+        stats = torch.zeros(2 * S * 2 * n, dtype=torch.float64, device=dev)
+        for label, mode, drop, want_stats in [("raw", 0, 0.0, False), ("raw+stats", 0, 0.0, True),
+                                              ("bn", 1, 0.0, False), ("bn-eval", 2, 0.0, False),
+                                              ("bn+drop", 1, 0.2, False), ("bn+drop+stats", 1, 0.2, True)]:
+            a = LinearFwdArgs()
+            a.src, a.src_rows, a.ld_src, a.m, a.k, a.n = src.data_ptr(), m, k, m, k, n
+            a.w, a.bias, a.z_out, a.act = w.data_ptr(), b.data_ptr(), z.data_ptr(), 0
+            a.prev_mode, a.prev_act = mode, 0
+            if mode:
+                a.prev_stats, a.bn_gamma, a.bn_beta = stats_prev.data_ptr(), gam.data_ptr(), bet.data_ptr()
+                a.running_mean, a.running_var = rm.data_ptr(), rv.data_ptr()
+                a.save_mean, a.save_invstd = sm.data_ptr(), si.data_ptr()
+                a.bn_eps, a.bn_momentum = 1e-5, 0.1
+                a.seg_split = 1024
+            a.drop_p, a.drop_seed = drop, 7
+            if want_stats:
+                a.stats_out = stats.data_ptr()
+            us = timeit(lambda: call("rt_linear_fwd_f32", ctypes.byref(a), st))
+            print(f"fwd m={m:5d} blocks={m // 32:4d} {label:14s} {us:8.1f} us {2 * m * k * n / us / 1e6:7.2f} TF/s")
+
+
 def split_bwd():
     """dz and dW launches timed separately at the C2 item-tower shapes (17,408
     rows), hidden-layer form, with and without the dropout prologue."""
@@ -190,5 +232,8 @@ if __name__ == "__main__":
     elif "--fwd-epi" in sys.argv:
         native.lib()
         fwd_epilogues()
+    elif "--fwd-attr" in sys.argv:
+        native.lib()
+        fwd_attr()
     else:
         main()
