@@ -7,13 +7,15 @@
 // num_negatives the whole pool is returned (here: in increasing id order, the
 // remaining slots = -1).
 //
-// One wave per batch row. Lane j owns negative slot j: it proposes a
-// counter-hashed item, rejects it if it is one of the user's positives
-// (binary search in the user's sorted CSR segment) or equals an accepted slot or
-// a lower lane's same-round proposal, and retries until every slot holds a value.
+// One wave per batch row, proposals counter-hashed from (seed, row, round, lane).
+// Catalogues up to 65,536 items keep the user's positives and the accepted
+// negatives in a per-wave LDS bitmap: all 64 lanes propose each round and the
+// proposals whose bit they set first fill the open slots in lane order.
+// Larger catalogues: lane j owns slot j, rejects a proposal that is one of the
+// user's positives (binary search in the user's sorted CSR segment) or equals
+// an accepted slot or a lower lane's same-round proposal, and retries.
 // Distinctness is exact; the accepted set is uniform over the pool because each
 // round's proposals are uniform and rejection only removes forbidden values.
-// Catalogues up to 65,536 items test membership in a per-wave LDS bitmap.
 #include "rt_common.h"
 
 namespace rt {
@@ -69,9 +71,19 @@ __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __
     if constexpr (BITMAP) {
         for (int i = lane; i < words; i += 64) bits[i] = 0u;
         wave_lds_sync();
-        for (int64_t i = lo + lane; i < hi; i += 64) {
-            const int32_t it = items[i];
-            if (it >= 0 && it < num_items) atomicOr(&bits[it >> 5], 1u << (it & 31));
+        // kPosUnroll independent loads per lane in flight before their LDS ors:
+        // a heavy user's ~2,300 positives take 5 load round trips, not 37
+        constexpr int kPosUnroll = 8;
+        for (int64_t base = lo; base < hi; base += 64 * kPosUnroll) {
+            int32_t v[kPosUnroll];
+#pragma unroll
+            for (int k = 0; k < kPosUnroll; ++k) {
+                const int64_t i = base + k * 64 + lane;
+                v[k] = i < hi ? items[i] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < kPosUnroll; ++k)
+                if (v[k] >= 0 && v[k] < num_items) atomicOr(&bits[v[k] >> 5], 1u << (v[k] & 31));
         }
         wave_lds_sync();
     }
@@ -91,6 +103,29 @@ __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __
             written += __popcll(m);
         }
         for (int j = (written < num_neg ? written : num_neg) + lane; j < num_neg; j += 64) o[j] = -1;
+        return;
+    }
+    if constexpr (BITMAP) {
+        // Every lane proposes each round. A proposal is taken when its bit was
+        // clear at its LDS or-with-return: positives and earlier-accepted
+        // negatives are already set, and of equal proposals in one round only
+        // the first to reach the LDS sees the bit clear. Taken proposals fill
+        // the open slots in lane order; a round's surplus is dropped. Read in
+        // (round, lane) order this is sequential uniform draws without
+        // replacement from the pool, so the sample is uniform; a heavy user
+        // (a third of the catalogue left) fills 16 slots in one round.
+        int filled = 0;
+        for (int round = 0; round < kMaxRounds && filled < num_neg; ++round) {
+            const uint32_t r = draw(sd, row, round, lane);
+            const int32_t c = static_cast<int32_t>((static_cast<uint64_t>(r) * static_cast<uint64_t>(num_items)) >> 32);
+            const uint32_t bit = 1u << (c & 31);
+            const bool ok = (atomicOr(&bits[c >> 5], bit) & bit) == 0u;
+            const uint64_t m = __ballot(ok);
+            const int slot = filled + __popcll(m & ((1ull << lane) - 1ull));
+            if (ok && slot < num_neg) o[slot] = c;
+            filled += __popcll(m);
+        }
+        for (int j = (filled < num_neg ? filled : num_neg) + lane; j < num_neg; j += 64) o[j] = -1;
         return;
     }
     int32_t mine = -1;
