@@ -113,6 +113,23 @@ def test_feeder_batches(device):
     assert n == len(f) > 0
 
 
+def test_sampler_heavy_users(device):
+    """Users holding most of the catalogue (the LDS bitmap path's many-rejection
+    case) and a few thousand positives each: exact contract at pools of 17..400."""
+    rng = np.random.default_rng(4)
+    num_items, num_neg = 3416, 16
+    its = [np.sort(rng.choice(num_items, num_items - p, replace=False)) for p in (17, 40, 400, 1200)]
+    csr = PositiveCSR.from_pairs(np.concatenate([np.full(len(x), u) for u, x in enumerate(its)]),
+                                 np.concatenate(its), len(its))
+    dcsr = csr.to(device)
+    users = torch.from_numpy(rng.integers(0, len(its), 3000)).to(device)
+    o = kernels.sample_negatives(dcsr.offsets, dcsr.items, users, num_items, num_neg, seed=21).cpu().numpy()
+    for r, u in enumerate(users.cpu().numpy()):
+        row = o[r]
+        assert len(set(row.tolist())) == num_neg and ((row >= 0) & (row < num_items)).all()
+        assert not set(row.tolist()) & set(its[u].tolist())
+
+
 def test_id_batches_equal_dense_batches(device):
     from rtrec_amd.training.fused_step import FusedTrainStep
     from rtrec_amd.training.utils import create_two_tower_model_for_training
