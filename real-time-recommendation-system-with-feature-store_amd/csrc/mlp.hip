@@ -1059,8 +1059,10 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     // staging columns cn (lanes l ^ 16·j when VN = 16, l ^ 32 when VN = 32) are
     // summed by shuffles, the 8 waves through LDS, then ONE atomic per column
     // per block (same-address float atomics serialise: 8 per block measured
-    // 40-80 µs at the C2 shapes). Row group 1 hands its accumulators to group 0
-    // through the (idle) dz buffers, the dbias partials go through the A buffers.
+    // 40-80 µs at the C2 shapes). Each row group adds half of the dW tile and
+    // hands the other half of its accumulators to the other group through the
+    // (idle) dz buffers (both groups issue atomics: 1.5 µs/step faster than
+    // group 0 adding all of it); the dbias partials go through the A buffers.
     float* red = &Ld[0][0];
     float* bred = &La[0][0];  // [8 waves][VN][4]
     if (do_bias) {
@@ -1073,12 +1075,12 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         }
         if (lane < VN) *reinterpret_cast<float4*>(&bred[(wg * VN + lane) * 4]) = bsum;
     }
-    if (grp == 1) {
+    // row group grp adds accumulator rows 8·grp .. 8·grp+7 of the tile
 #pragma unroll
-        for (int t = 0; t < T; ++t)
+    for (int t = 0; t < T; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) red[((w * T + t) * 16 + r) * 64 + lane] = acc[t][r];
-    }
+        for (int r = 0; r < 16; ++r)
+            if ((r >> 3) != grp) red[((w * T + t) * 16 + r) * 64 + lane] = acc[t][r];
     __syncthreads();
     if (do_bias && tid < VN) {
         float4 sb = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1093,18 +1095,19 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         if (cb + 2 < n) atomicAdd(&a.dbias[cb + 2], sb.z);
         if (cb + 3 < n) atomicAdd(&a.dbias[cb + 3], sb.w);
     }
-    if (grp == 1) return;
     // acc[t][r] = dW[n0 + ncol-tile + (r&3) + 8(r>>2) + 4h][k0 + kcol0 + 32t]
+    auto add_row = [&](int t, int r, int kk) {
+        const int nn = n0 + (w % NTN) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float v = acc[t][r] + red[((w * T + t) * 16 + r) * 64 + lane];
+        if (nn < n) atomicAdd(&a.dw[static_cast<int64_t>(nn) * k + kk], v);
+    };
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int kk = k0 + kcol0 + 32 * t;
         if (kk >= k) continue;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int nn = n0 + (w % NTN) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const float v = acc[t][r] + red[((w * T + t) * 16 + r) * 64 + lane];
-            if (nn < n) atomicAdd(&a.dw[static_cast<int64_t>(nn) * k + kk], v);
-        }
+        for (int r = 0; r < 16; ++r)
+            if ((r >> 3) == grp) add_row(t, r, kk);
     }
 }
 
