@@ -69,18 +69,24 @@ inline Shape shape_for(int dtype, int d, int k) {
     return dtype == RT_F32 ? shape_f32(d, k) : dtype == RT_F16 ? shape_f16(d, k) : shape_bf16(d, k);
 }
 
+constexpr int64_t kCUs = 256;  // MI355X compute units
+
 inline Plan make_plan(int64_t nq, int64_t nx, int k, const Shape& sh) {
     Plan p{};
     p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
     if (p.chunk < 1) p.chunk = 1;
     p.q_tiles = static_cast<int>((p.chunk + sh.qt - 1) / sh.qt);
-    // ~2 blocks per CU (512), but keep >= 4 item tiles per split
     const int64_t tiles = (nx + sh.nt - 1) / sh.nt;
     int64_t splits;
     if (sh.kind == 2) {
         splits = v2::planned_splits(p.q_tiles, nx);
     } else {
-        splits = (512 + p.q_tiles - 1) / p.q_tiles;
+        // at most 2 blocks per CU (<= 512 blocks: one co-resident wave of
+        // blocks, no tail), >= 4 item tiles per split, <= 64 splits. C3 (48
+        // query tiles x 54 item tiles): 9 splits = 432 blocks run 0.217 ms;
+        // rounding up to 11 splits = 528 blocks (3 on some CUs) ran 0.244 ms,
+        // 14 splits = 672 blocks 0.243 ms.
+        splits = 2 * kCUs / p.q_tiles;
         int64_t max_splits = tiles / 4;
         if (max_splits < 1) max_splits = 1;
         if (splits > max_splits) splits = max_splits;
