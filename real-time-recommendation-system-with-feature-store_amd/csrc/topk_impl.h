@@ -224,15 +224,25 @@ __global__ __launch_bounds__(256) void flatip_topk_kernel(Args a, int64_t items_
                 for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[j][r]);
                 if (__ballot(mx > th[j]) == 0) continue;  // wave-uniform skip
                 const f32x16 aj = acc[j];
-                // rolled on purpose (one copy of the insertion code; dynamic extract)
-#pragma unroll 1
-                for (int r = 0; r < 16; ++r) {
-                    const float v = aj[r];
-                    if (v > th[j]) {
+                // per-lane pass mask; the wave loops max-popcount times (not 16),
+                // each lane taking its passing rows in increasing r (= id) order,
+                // the order of the plain r loop, so the lists come out the same
+                uint32_t bits = 0u;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) bits |= (aj[r] > th[j] ? 1u : 0u) << r;
+                while (__ballot(bits != 0u)) {
+                    if (bits) {
+                        const int r = __builtin_ctz(bits);
+                        bits &= bits - 1u;
+                        float v = aj[0];
+#pragma unroll
+                        for (int rr = 1; rr < 16; ++rr) v = (r == rr) ? aj[rr] : v;
                         const uint32_t item = static_cast<uint32_t>(sub0 + tile_row(r, half));
-                        if (excl[j] && ((excl[j][item >> 5] >> (item & 31)) & 1u)) continue;
-                        list_insert<K>(ls[j], li[j], v, item);
-                        th[j] = ls[j][K - 1];
+                        const bool ex = excl[j] && ((excl[j][item >> 5] >> (item & 31)) & 1u);
+                        if (v > th[j] && !ex) {
+                            list_insert<K>(ls[j], li[j], v, item);
+                            th[j] = ls[j][K - 1];
+                        }
                     }
                 }
             }
