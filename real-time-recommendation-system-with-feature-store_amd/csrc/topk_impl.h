@@ -123,8 +123,33 @@ __device__ __forceinline__ void list_insert(float (&ls)[K], uint32_t (&li)[K], f
     }
 }
 
+// bitonic sort of N (a power of two) register entries of one lane, better first
+template <int N>
+__device__ __forceinline__ void lane_sort(float (&s)[N], uint32_t (&id)[N]) {
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                if ((i & stride) == 0) {
+                    const int j = i | stride;
+                    const bool up = (i & size) == 0;
+                    if (better(s[j], id[j], s[i], id[i]) == up) {
+                        const float ts = s[i];
+                        const uint32_t ti = id[i];
+                        s[i] = s[j];
+                        id[i] = id[j];
+                        s[j] = ts;
+                        id[j] = ti;
+                    }
+                }
+            }
+}
+
 template <typename T, int S, int K>
-__global__ __launch_bounds__(256) void flatip_topk_kernel(Args a, int64_t items_per_split) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void flatip_topk_kernel(Args a,
+                                                                                       int64_t items_per_split) {
     using M = Mfma<T>;
     using C = Cfg<T, S, K>;
     constexpr int KK = C::KK, QS = C::QS, QT = C::QT, NT = C::NT, LS = C::LS, VEC = C::VEC, DP = C::DP;
@@ -224,6 +249,29 @@ __global__ __launch_bounds__(256) void flatip_topk_kernel(Args a, int64_t items_
                 for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[j][r]);
                 if (__ballot(mx > th[j]) == 0) continue;  // wave-uniform skip
                 const f32x16 aj = acc[j];
+                if (t0 == i_begin && rt == 0) {
+                    // the split's first sub-tile meets empty lists: one sort of
+                    // the lane's 16 rows gives the list 16 in-order inserts
+                    // would build (rows that would not insert become empties)
+                    float s16[16];
+                    uint32_t i16[16];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const uint32_t item = static_cast<uint32_t>(sub0 + tile_row(r, half));
+                        bool ok = qok[j] && aj[r] > th[j];
+                        if (ok && excl[j]) ok = !((excl[j][item >> 5] >> (item & 31)) & 1u);
+                        s16[r] = ok ? aj[r] : -INFINITY;
+                        i16[r] = ok ? item : kEmptyId;
+                    }
+                    lane_sort<16>(s16, i16);
+#pragma unroll
+                    for (int i = 0; i < K; ++i) {
+                        ls[j][i] = i < 16 ? s16[i < 16 ? i : 0] : -INFINITY;
+                        li[j][i] = i < 16 ? i16[i < 16 ? i : 0] : kEmptyId;
+                    }
+                    if (qok[j]) th[j] = ls[j][K - 1];
+                    continue;
+                }
                 // per-lane pass mask; the wave loops max-popcount times (not 16),
                 // each lane taking its passing rows in increasing r (= id) order,
                 // the order of the plain r loop, so the lists come out the same
