@@ -98,6 +98,10 @@ class ParamSlab:
         self.grad: Optional[torch.Tensor] = None
         self.offsets: List[int] = []
         self.offsets_dev: Optional[torch.Tensor] = None
+        # bumped whenever something outside the fused step may have written the
+        # grad slab (autograd backward through attach_grads, a slab rebuild);
+        # FusedTrainStep re-zeroes the slab before its next step when it changes
+        self.grad_gen = 0
 
     def _valid(self) -> bool:
         ps = [p for p in self.module.parameters()]
@@ -137,6 +141,7 @@ class ParamSlab:
             if old is not None:
                 p.grad.copy_(old)
         self.params, self.offsets, self.data, self.grad = ps, offs, data, grad
+        self.grad_gen += 1
         self.__dict__["_grad_views"] = {}
         ends = [o + s for o, s in zip(offs, sizes)]
         self.bounds = list(zip(offs, ends))
@@ -144,8 +149,10 @@ class ParamSlab:
         return self
 
     def attach_grads(self):
-        """Make every param's .grad the slab view again (after zero_grad(set_to_none))."""
+        """Make every param's .grad the slab view again (after zero_grad(set_to_none)).
+        Called by every autograd backward that accumulates into the slab."""
         self.ensure()
+        self.grad_gen += 1
         for p, (o, e) in zip(self.params, self.bounds):
             view = self.grad[o:e]
             if p.grad is None:

@@ -68,6 +68,11 @@ class FusedTrainStep:
         self.small = torch.zeros(3 + len(self.slab.params), dtype=torch.float64, device=dev)
         self.loss_buf, self.sumsq = self.small[:3], self.small[3:]
         self.slab.grad.zero_()  # the step owns the grad slab from here on (consumed by clip+Adam)
+        # the step relies on the previous clip+Adam having zeroed the grad slab
+        # and the stats arena; that holds only while nothing else wrote the slab
+        # (an autograd backward bumps slab.grad_gen) and the last step finished
+        self._clean = True
+        self._grad_gen = self.slab.grad_gen
         # the pos and neg arenas are adjacent: together they are the [2]-segment
         # arena of the merged item chain
         self.a_pqf = self.arena[ua:ua + 2 * ia]
@@ -122,10 +127,23 @@ class FusedTrainStep:
         self.set_lr(float(sd["param_groups"][0]["lr"]))
 
     # ------------------------------------------------------------------
+    def _ensure_clean(self):
+        """Zero the grad slab and the fp64 stats arena when a previous step did
+        not finish or an autograd backward accumulated into the slab since (the
+        common path is memset-free: clip+Adam zeroes what it consumes)."""
+        if not self._clean or self.slab.grad_gen != self._grad_gen:
+            self.slab.grad.zero_()
+            self.arena.zero_()
+            self._grad_gen = self.slab.grad_gen
+        self._clean = False
+
     def _run(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None):
+        self._ensure_clean()
         self._grads(user_src, pos_src, neg_src, user_ids, pos_ids, neg_ids)
         self._allreduce()
-        return self._update()
+        out = self._update()
+        self._clean = True
+        return out
 
     def _grads(self, user_src, pos_src, neg_src, user_ids=None, pos_ids=None, neg_ids=None):
         """Forward, fused loss, backward: parameter grads in the slab."""
@@ -279,10 +297,12 @@ class FusedTrainStep:
         return g
 
     def replay(self):
+        self._ensure_clean()
         self.graph.replay()
         if self.graph_update is not None:
             self._allreduce()
             self.graph_update.replay()
+        self._clean = True
         self.steps += 1
         return self.loss_buf
 

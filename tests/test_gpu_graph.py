@@ -104,3 +104,31 @@ def test_two_graph_data_parallel_capture(device):
         _check(m1, m2, ref, got)
     finally:
         dist.destroy_process_group()
+
+
+def test_step_after_autograd_backward_matches_fresh_step(device):
+    """an autograd backward through the same model between fused
+    steps accumulates into the shared grad slab. The next fused step must see a
+    clean slab (it re-zeroes when slab.grad_gen moved), so it equals the same
+    step on an untouched copy of the model."""
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    ut, mt, batches, m1 = _setup(device)
+    m2 = copy.deepcopy(m1)
+    s1, s2 = FusedTrainStep(m1), FusedTrainStep(m2)
+    b = batches[0]
+    s1(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2])
+    s2(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2])
+    # autograd through the HIP towers of m1 only: grads land in m1's slab
+    m1.train()
+    u = m1.user_tower(ut[:64].contiguous())
+    p = m1.item_tower(mt[:64].contiguous())
+    m1.in_batch_negative_loss(u, p).backward()
+    assert float(s1.slab.grad.abs().sum()) > 0.0
+    # BN running stats moved in m1's towers: copy them over so only the slab differs
+    with torch.no_grad():
+        for a, c in zip(m2.buffers(), m1.buffers()):
+            a.copy_(c)
+    b = batches[1]
+    ref = s2(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone()
+    got = s1(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone()
+    _check(m2, m1, [ref], [got])
