@@ -92,18 +92,31 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
                    float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* Planner override of rt_flatip_topk (tests and tuning; process-wide, not
+ * thread-safe, results unchanged by any setting). v4_mode: 0 automatic, 1 never
+ * the sampled-threshold kernel pair, 2 it wherever legal (16-bit, d <= 128,
+ * k <= 128). v4_stride: sample every stride-th 128-row stage (0 = planner).
+ * v4_rank: threshold = rank-th largest sampled group maximum (-1 = planner,
+ * 0 = no sample: a running threshold from -inf). Set before sizing the
+ * workspace. */
+int rt_flatip_topk_tuning(int v4_mode, int v4_stride, int v4_rank);
+
 /* IndexFlatL2 mode (FaissIndex with metric != "cosine", src/serving/retrieval.py:
  * 96-100). rt_l2_augment_f32 writes rows [x, a, 0...] of ld_out >= d + 1 floats:
- * a = 1 for queries (role 0), a = -0.5*||x||^2 for items (role 1); then
- * rt_flatip_topk on the augmented rows (d' = ld_out) ranks items by
- * q.x - ||x||^2/2, i.e. by ascending ||q - x||^2. rt_l2_finish_f32 rewrites each
- * [nq, k] result row (ids = item index + id_offset into x_aug) with Faiss's
- * reported distance (||q||^2 + ||x||^2 - 2 q.x over the first d columns,
- * sequential fmaf norms and dot, clamped at 0) re-sorted by (distance asc, id
- * asc); unfilled slots (FLT_MAX, -1). k <= 512. */
+ * a = 1 for queries (role 0), a = -0.5*||x||^2 for items (role 1; ||x||^2 a
+ * sequential fmaf chain); then rt_flatip_topk on the augmented rows (d' =
+ * ld_out) ranks items by q.x - ||x||^2/2, i.e. by ascending ||q - x||^2.
+ * rt_l2_finish_f32 takes k_sel >= k such candidates per query (sel_ids
+ * [nq, k_sel], item index + id_offset into x_aug, -1 = none) and writes the k
+ * nearest by Faiss's reported distance (||q||^2 + ||x||^2 - 2 q.x over the first
+ * d columns, sequential fmaf norms and dot, clamped at 0), sorted by (distance
+ * asc, id asc), into scores/ids [nq, k]; unfilled slots (FLT_MAX, -1). The
+ * selection score and the reported distance round differently: exact (equal to
+ * Faiss) unless more than k_sel - k items lie within rounding of the k-th
+ * distance. k_sel <= 512; sel_ids may alias ids only when k_sel == k. */
 int rt_l2_augment_f32(const float* x, int64_t n, int d, float* out, int ld_out, int role, void* stream);
-int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq, int k,
-                     float* scores, int64_t* ids, int64_t id_offset, void* stream);
+int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq, int k_sel,
+                     const int64_t* sel_ids, int k, float* scores, int64_t* ids, int64_t id_offset, void* stream);
 
 /* Merge n_lists candidate lists per query, layout [n_lists][nq][k_in] (as an
  * all_gather_into_tensor over ranks produces), into the (score desc, id asc)

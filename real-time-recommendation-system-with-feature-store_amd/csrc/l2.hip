@@ -4,13 +4,18 @@
 //
 // Ranking ‖q − x‖² ascending equals ranking q·x − ½‖x‖² descending, so both
 // sides are AUGMENTED once (rt_l2_augment_f32): item rows [x, −½‖x‖², 0, 0, 0],
-// query rows [q, 1, 0, 0, 0] (d + 4 columns, 16-byte rows), and
-// rt_flatip_topk selects on the augmented inner product. rt_l2_finish_f32 then
-// recomputes the reported distance of every selected item exactly as Faiss's
-// BLAS path defines it (exhaustive_L2sqr_blas: ‖q‖² + ‖x‖² − 2·q·x, clamped at
-// 0; norms and the dot as sequential fmaf chains, the order oracle/flatip.c
-// uses) and re-sorts each list by (distance asc, id asc) — Faiss's max-heap
-// keeps the lower id on exact ties. Unfilled slots: (FLT_MAX, −1).
+// query rows [q, 1, 0, 0, 0] (d + 4 columns, 16-byte rows; ‖x‖² a sequential
+// fmaf chain, the oracle's order), and rt_flatip_topk selects k_sel >= k
+// candidates on the augmented inner product. rt_l2_finish_f32 then recomputes
+// the reported distance of every candidate exactly as Faiss's BLAS path
+// defines it (exhaustive_L2sqr_blas: ‖q‖² + ‖x‖² − 2·q·x, clamped at 0; norms
+// and the dot as sequential fmaf chains, the order oracle/flatip.c uses),
+// re-sorts by (distance asc, id asc) — Faiss's max-heap keeps the lower id on
+// exact ties — and keeps the k best. The augmented score and the reported
+// distance round differently, so items can swap order near the k-th distance;
+// the k_sel − k extra candidates (32 in kernels.flatl2_topk) absorb that: the
+// result is Faiss's unless more than k_sel − k items sit within rounding of the
+// k-th distance. Unfilled slots: (FLT_MAX, −1).
 #include <float.h>
 
 #include "rt_common.h"
@@ -27,13 +32,11 @@ __global__ __launch_bounds__(256) void augment_kernel(const float* __restrict__ 
     if (r >= n) return;
     const float* xr = x + r * d;
     float* o = out + r * ld_out;
-    float ss = 0.f;
-    for (int c = lane; c < d; c += 64) {
-        const float v = xr[c];
-        o[c] = v;
-        ss = __builtin_fmaf(v, v, ss);
-    }
-    ss = wave_sum(ss);
+    for (int c = lane; c < d; c += 64) o[c] = xr[c];
+    float ss = 0.f;  // ||x||^2 in the finish pass's (and the oracle's) sequential order
+    if (role == 1 && lane == 0)
+        for (int c = 0; c < d; ++c) ss = __builtin_fmaf(xr[c], xr[c], ss);
+    ss = __shfl(ss, 0, 64);
     for (int c = d + lane; c < ld_out; c += 64) o[c] = (c == d) ? (role == 0 ? 1.f : -0.5f * ss) : 0.f;
 }
 
@@ -45,10 +48,11 @@ __device__ __forceinline__ float seq_dot(const float* __restrict__ a, const floa
 
 constexpr int kFinishN = 512;  // entries per wave (k <= 512)
 
-// one wave per query: exact distances of the k selected items, re-sorted
+// one wave per query: exact distances of the k_sel candidates, re-sorted, k kept
 __global__ __launch_bounds__(256) void finish_kernel(const float* __restrict__ q_aug, int ld_q,
                                                      const float* __restrict__ x_aug, int ld_x, int d, int64_t nq,
-                                                     int k, float* __restrict__ scores, int64_t* __restrict__ ids,
+                                                     int k_sel, const int64_t* __restrict__ sel_ids, int k,
+                                                     float* __restrict__ scores, int64_t* __restrict__ ids,
                                                      int64_t id_offset) {
     __shared__ Cand buf[4][kFinishN];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -56,12 +60,12 @@ __global__ __launch_bounds__(256) void finish_kernel(const float* __restrict__ q
     if (q >= nq) return;  // wave-uniform; only wave-level LDS sync below
     const float* qr = q_aug + q * ld_q;
     const float qn = seq_dot(qr, qr, d);
-    const int n = next_pow2(k < 2 ? 2 : k);
+    const int n = next_pow2(k_sel < 2 ? 2 : k_sel);
     Cand* b = buf[w];
     for (int e = lane; e < n; e += 64) {
         Cand c{-INFINITY, kEmptyId};
-        if (e < k) {
-            const int64_t id = ids[q * k + e];
+        if (e < k_sel) {
+            const int64_t id = sel_ids[q * k_sel + e];
             if (id >= 0) {
                 const int64_t pos = id - id_offset;
                 const float* xr = x_aug + pos * ld_x;
@@ -98,13 +102,15 @@ extern "C" int rt_l2_augment_f32(const float* x, int64_t n, int d, float* out, i
     return check_launch("l2_augment_kernel");
 }
 
-extern "C" int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq, int k,
-                                float* scores, int64_t* ids, int64_t id_offset, void* stream) {
-    if (nq < 0 || d <= 0 || k <= 0 || ld_q < d || ld_x < d || id_offset < 0) return RT_ERR_INVALID;
-    if (k > l2::kFinishN) return RT_ERR_UNSUPPORTED;
+extern "C" int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq,
+                                int k_sel, const int64_t* sel_ids, int k, float* scores, int64_t* ids,
+                                int64_t id_offset, void* stream) {
+    if (nq < 0 || d <= 0 || k <= 0 || k_sel < k || ld_q < d || ld_x < d || id_offset < 0) return RT_ERR_INVALID;
+    if (k_sel > l2::kFinishN) return RT_ERR_UNSUPPORTED;
     if (nq == 0) return RT_OK;
-    if (!q_aug || !x_aug || !scores || !ids) return RT_ERR_INVALID;
+    if (!q_aug || !x_aug || !sel_ids || !scores || !ids) return RT_ERR_INVALID;
+    if (sel_ids == ids && k_sel != k) return RT_ERR_INVALID;  // in place only without over-selection
     hipLaunchKernelGGL(l2::finish_kernel, dim3(static_cast<unsigned>((nq + 3) / 4)), dim3(256), 0, as_stream(stream),
-                       q_aug, ld_q, x_aug, ld_x, d, nq, k, scores, ids, id_offset);
+                       q_aug, ld_q, x_aug, ld_x, d, nq, k_sel, sel_ids, k, scores, ids, id_offset);
     return check_launch("l2_finish_kernel");
 }

@@ -43,8 +43,11 @@ __device__ __forceinline__ bool contains(const int32_t* __restrict__ items, int6
 // BITMAP: the catalogue fits a per-wave LDS bitmap (num_items <= kMaxBitmapItems):
 // the user's positives are set in it once, accepted negatives are added as
 // they are taken, so every membership test is one LDS read instead of a
-// dependent binary search through global memory. Same draws, same acceptance
-// rule, same output as the search form.
+// dependent binary search through global memory. The two forms do NOT produce
+// the same negatives for the same seed: the bitmap form has all 64 lanes
+// propose every round and fills the open slots in lane order (the surplus
+// dropped), the search form has lane j own slot j. Both guarantee only the
+// contract: distinct negatives, none a positive, uniform over the rest.
 constexpr int64_t kMaxBitmapItems = 65536;
 
 template <bool BITMAP>

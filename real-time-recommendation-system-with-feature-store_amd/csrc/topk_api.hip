@@ -1,6 +1,8 @@
 // C ABI for the Flat-IP top-K (rt_flatip_topk) and the candidate-list merge
 // (rt_topk_merge, used for split corpora and for the multi-GPU merge of
 // per-shard top-K lists after an RCCL all-gather).
+#include <cmath>
+
 #include "topk_impl.h"
 
 namespace rt {
@@ -116,8 +118,89 @@ inline Shape shape_for(int dtype, int d, int k) {
 
 constexpr int64_t kCUs = 256;  // MI355X compute units
 
-inline Plan make_plan(int64_t nq, int64_t nx, int k, const Shape& sh) {
+// planner overrides for tests and tuning (rt_flatip_topk_tuning)
+static int g_v4_mode = 0;     // 0 auto, 1 never, 2 wherever legal
+static int g_v4_stride = 0;   // 0: planner's choice
+static int g_v4_rank = -1;    // -1: planner's choice; 0: no sample (v2-style running threshold)
+
+// log P(Bin(n, f) >= r)
+inline double log_binom_tail(int n, double f, int r) {
+    if (r <= 0) return 0.0;
+    if (r > n) return -1e300;
+    double acc = 0.0;
+    bool any = false;
+    double mx = -1e300;
+    double terms[kMaxK + 1];
+    for (int i = r; i <= n; ++i) {
+        const double t = std::lgamma(n + 1.0) - std::lgamma(i + 1.0) - std::lgamma(n - i + 1.0) + i * std::log(f) +
+                         (n - i) * std::log1p(-f);
+        terms[i] = t;
+        if (t > mx) mx = t;
+        any = true;
+    }
+    if (!any) return -1e300;
+    for (int i = r; i <= n; ++i) acc += std::exp(terms[i] - mx);
+    return mx + std::log(acc);
+}
+
+// the v4 sample: the sparsest stride whose smallest safe rank keeps the expected
+// candidates per (split, query) near rank/f <= ~360. "Safe": the estimate
+// overshoots the split's k-th score (a rescan) with probability <= 1e-6 —
+// P(>= rank of the split's top k fall in the sample) for a 1/f sample; the
+// group-maximum estimate sits at or below the item rank, so this bounds it.
+inline void plan_v4_sample(int k, int64_t items_per_split, int& stride, int& rank) {
+    const int64_t nst = (items_per_split + v4::Cfg4<__half, 8>::NT - 1) / v4::Cfg4<__half, 8>::NT;
+    stride = 0;
+    rank = 0;
+    for (int st = 64; st >= 2; --st) {
+        const int64_t nsa = (nst + st - 1) / st;
+        if (nsa < 4) continue;  // fewer than 32 groups per query in the sample
+        const double f = static_cast<double>(nsa) / static_cast<double>(nst);
+        for (int r = 1; r <= 2 * v4::kList; ++r) {
+            if (log_binom_tail(k, f, r) <= std::log(1e-6)) {
+                if (r / f <= 360.0) { stride = st; rank = r; return; }
+                break;
+            }
+        }
+    }
+}
+
+// v4 (sampled-threshold scan + finish) for 16-bit, d <= 128, 32 < k <= 128 over
+// a large corpus with enough queries to fill the chip at <= 8 item splits
+inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
+    if (g_v4_mode == 1) return false;
+    if (dtype == RT_F32 || d > 128 || k > v4::kMaxK) return false;
+    const bool forced = g_v4_mode == 2;
+    if (!forced && (k <= v3::kMaxKv3 || nx < 65536)) return false;
+    constexpr int QT = v4::Geo<2>::QT;
+    p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
+    if (p.chunk < 1) p.chunk = 1;
+    p.q_tiles = static_cast<int>((p.chunk + QT - 1) / QT);
+    if (!forced && p.q_tiles < 32) return false;
+    int splits = 1;
+    while (splits < v4::kMaxSplits && static_cast<int64_t>(p.q_tiles) * splits < kCUs) splits *= 2;
+    constexpr int NT = v4::Cfg4<__half, 8>::NT;
+    int64_t tiles = (nx + NT - 1) / NT;
+    while (splits > 1 && tiles / splits < 8) splits /= 2;
+    int64_t tiles_per = (tiles + splits - 1) / splits;
+    if (tiles_per < 1) tiles_per = 1;
+    p.items_per_split = tiles_per * NT;
+    p.splits = static_cast<int>(nx > 0 ? (nx + p.items_per_split - 1) / p.items_per_split : 1);
+    p.cap = v4::kCap;
+    p.v4 = 1;
+    plan_v4_sample(k, p.items_per_split, p.stride, p.rank);
+    if (g_v4_stride > 0) p.stride = g_v4_stride;
+    if (g_v4_rank >= 0) p.rank = g_v4_rank;
+    const int64_t q_pad = static_cast<int64_t>(p.q_tiles) * QT;
+    p.cand_bytes = static_cast<size_t>(p.splits) * q_pad * v4::kCap * sizeof(Cand);
+    p.meta_bytes = static_cast<size_t>(p.splits) * q_pad * 2 * sizeof(int);
+    p.part_bytes = 0;
+    return true;
+}
+
+inline Plan make_plan(int64_t nq, int64_t nx, int d, int dtype, int k, const Shape& sh) {
     Plan p{};
+    if (nx > 0 && plan_v4(nq, nx, d, dtype, k, p)) return p;
     p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
     if (p.chunk < 1) p.chunk = 1;
     p.q_tiles = static_cast<int>((p.chunk + sh.qt - 1) / sh.qt);
@@ -158,8 +241,8 @@ using namespace rt;
 extern "C" size_t rt_flatip_topk_workspace_bytes(int64_t nq, int64_t nx, int d, int dtype, int k) {
     if (nq <= 0 || k <= 0 || k > topk::kMaxK || d <= 0) return 256;
     if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return 256;
-    const topk::Plan p = topk::make_plan(nq, nx, k, topk::shape_for(dtype, d, k));
-    return topk::align256(p.cand_bytes) + p.part_bytes + 256;
+    const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
+    return topk::align256(p.cand_bytes) + p.part_bytes + topk::align256(p.meta_bytes) + 256;
 }
 
 extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
@@ -175,11 +258,12 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     if (nx >= 0xFFFFFFFFll || (id_offset + nx) >= 0xFFFFFFFFll || id_offset < 0) return RT_ERR_UNSUPPORTED;
     if ((reinterpret_cast<uintptr_t>(queries) | reinterpret_cast<uintptr_t>(items)) & 15) return RT_ERR_INVALID;
     if (exclude_bits && exclude_words < (nx + 31) / 32) return RT_ERR_INVALID;
-    const topk::Plan p = topk::make_plan(nq, nx, k, topk::shape_for(dtype, d, k));
+    const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
     const size_t cand_al = topk::align256(p.cand_bytes);
-    if (!workspace || workspace_bytes < cand_al + p.part_bytes) return RT_ERR_WORKSPACE;
+    if (!workspace || workspace_bytes < cand_al + p.part_bytes + topk::align256(p.meta_bytes)) return RT_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
     char* part = reinterpret_cast<char*>(workspace) + cand_al;
+    int* meta = reinterpret_cast<int*>(part + p.part_bytes);
     const size_t esz = dtype == RT_F32 ? 4 : 2;
     for (int64_t q0 = 0; q0 < nq; q0 += p.chunk) {
         const int64_t nc = (nq - q0) < p.chunk ? (nq - q0) : p.chunk;
@@ -202,7 +286,8 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
         a.excl_words = exclude_words;
         a.cand = reinterpret_cast<Cand*>(workspace);
         a.id_offset = id_offset;
-        if (p.splits > 1) {  // per-split lists [split][nc][k], merged below
+        a.meta = meta;
+        if (p.splits > 1 && !p.v4) {  // per-split lists [split][nc][k], merged below
             a.out_s = reinterpret_cast<float*>(part);
             a.out_i = reinterpret_cast<int64_t*>(part + static_cast<size_t>(p.splits) * p.chunk * k * sizeof(float));
         } else {
@@ -215,11 +300,20 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
             default: rc = topk::launch_bf16(a, p, st); break;
         }
         if (rc) return rc;
-        if (p.splits > 1) {
+        if (p.splits > 1 && !p.v4) {
             rc = topk::launch_merge(a.out_s, a.out_i, nc, p.splits, k, k, os, oi, st);
             if (rc) return rc;
         }
     }
+    return RT_OK;
+}
+
+extern "C" int rt_flatip_topk_tuning(int v4_mode, int v4_stride, int v4_rank) {
+    if (v4_mode < 0 || v4_mode > 2 || v4_stride < 0 || v4_rank < -1 || v4_rank > 2 * topk::v4::kList)
+        return RT_ERR_INVALID;
+    topk::g_v4_mode = v4_mode;
+    topk::g_v4_stride = v4_stride;
+    topk::g_v4_rank = v4_rank;
     return RT_OK;
 }
 

@@ -98,12 +98,16 @@ struct Plan {
     int64_t items_per_split;
     int cap;             // candidate buffer entries per query (v1 kernel), else 0
     size_t cand_bytes, part_bytes;
+    int v4;              // 1: the sampled-threshold scan + finish pair (topk_v4.h)
+    int stride, rank;    // v4 sample: every stride-th stage; threshold = rank-th group maximum
+    size_t meta_bytes;   // v4 per-(split, query, half) entry counts
 };
 
 struct Args {
     const void* Q; int64_t nq; const void* X; int64_t nx; int d; int k;
     const uint32_t* excl; int64_t excl_words;
     Cand* cand; float* out_s; int64_t* out_i; int64_t id_offset;
+    int* meta;
 };
 
 __device__ __forceinline__ int tile_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
@@ -359,6 +363,7 @@ int launch_cfg(const Args& a, const Plan& p, hipStream_t st) {
 #include "topk_v1.h"
 #include "topk_v2.h"
 #include "topk_v3.h"
+#include "topk_v4.h"
 
 namespace rt {
 namespace topk {
@@ -384,6 +389,9 @@ constexpr bool v2_fits() { return !(sizeof(T) == 4 && S > 64); }
 template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
     constexpr bool F32 = sizeof(T) == 4;
+    if constexpr (!F32 && S <= 8) {
+        if (p.v4) return v4::launch_S<T, S, 2>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank, a.meta, st);
+    }
     if constexpr (F32) {
         switch (list_k(true, a.k)) {
             case 16: return launch_cfg<T, S, 16>(a, p, st);

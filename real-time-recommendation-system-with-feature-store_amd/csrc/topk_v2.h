@@ -56,13 +56,14 @@ __device__ __forceinline__ float okey_inv(uint32_t k) {
 // One 8-bit radix step over the selected keys: the bin (of (key >> shift) & 255)
 // holding the kk-th largest selected key, and how many selected keys lie in
 // strictly higher bins. Whole wave calls; hist = this wave's 256 LDS words.
-__device__ inline void radix_bin(uint32_t* hist, const uint32_t (&key)[kE], const bool (&sel)[kE], int shift,
+template <int E = kE>
+__device__ inline void radix_bin(uint32_t* hist, const uint32_t (&key)[E], const bool (&sel)[E], int shift,
                                  int kk, int& bin, int& above) {
     const int lane = threadIdx.x & 63;
     reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
     wave_lds_sync();
 #pragma unroll
-    for (int e = 0; e < kE; ++e)
+    for (int e = 0; e < E; ++e)
         if (sel[e]) atomicAdd(&hist[(key[e] >> shift) & 255u], 1u);
     wave_lds_sync();
     const uint4 h = reinterpret_cast<const uint4*>(hist)[lane];
@@ -88,15 +89,19 @@ __device__ inline void radix_bin(uint32_t* hist, const uint32_t (&key)[kE], cons
 
 // entry idx of a query buffer holding n0 entries in its first half and the
 // rest in its second
+template <int HALF = kHalf>
 __device__ __forceinline__ const Cand& entry(const Cand* buf, int n0, int idx) {
-    return idx < n0 ? buf[idx] : buf[kHalf + (idx - n0)];
+    return idx < n0 ? buf[idx] : buf[HALF + (idx - n0)];
 }
 
 // Shrink one query's buffer (halves of n0 and n1 entries, k <= n0+n1) to a
 // superset of its top k, re-dealt over the halves (entry j → half j&1, slot
 // j>>1). Returns the new total; thr = the new filter threshold (v >= thr).
-__device__ __noinline__ int compact_query(Cand* __restrict__ buf, int n0, int n1, int k, uint32_t* hist,
-                                          float& thr) {
+// CAP = the buffer's entry capacity (v2/v3: kCap; v4: its own).
+template <int CAP = kCap>
+__device__ __forceinline__ int compact_query_body(Cand* __restrict__ buf, int n0, int n1, int k, uint32_t* hist,
+                                                  float& thr) {
+    constexpr int kE = CAP / 64, kHalf = CAP / 2, kCap = CAP;
     const int lane = threadIdx.x & 63;
     const int n = n0 + n1;
     float s[kE];
@@ -106,17 +111,17 @@ __device__ __noinline__ int compact_query(Cand* __restrict__ buf, int n0, int n1
     for (int e = 0; e < kE; ++e) {
         const int idx = e * 64 + lane;
         sel[e] = idx < n;
-        const Cand c = sel[e] ? entry(buf, n0, idx) : Cand{-INFINITY, kEmptyId};
+        const Cand c = sel[e] ? entry<kHalf>(buf, n0, idx) : Cand{-INFINITY, kEmptyId};
         s[e] = c.s;
         id[e] = c.i;
         key[e] = okey(c.s);
     }
     int b1, a1, b2, a2;
-    radix_bin(hist, key, sel, 24, k, b1, a1);
+    radix_bin<kE>(hist, key, sel, 24, k, b1, a1);
     bool sel2[kE];
 #pragma unroll
     for (int e = 0; e < kE; ++e) sel2[e] = sel[e] && (key[e] >> 24) == static_cast<uint32_t>(b1);
-    radix_bin(hist, key, sel2, 16, k - a1, b2, a2);
+    radix_bin<kE>(hist, key, sel2, 16, k - a1, b2, a2);
     const uint32_t T = (static_cast<uint32_t>(b1) << 24) | (static_cast<uint32_t>(b2) << 16);
     bool keep[kE];
     int total = 0;
@@ -155,6 +160,12 @@ __device__ __noinline__ int compact_query(Cand* __restrict__ buf, int n0, int n1
     thr = nextafterf(kth, INFINITY);
     __threadfence_block();
     return k;
+}
+// out of line (v2/v3 scans: keeps the compaction's registers out of the loop)
+template <int CAP = kCap>
+__device__ __noinline__ int compact_query(Cand* __restrict__ buf, int n0, int n1, int k, uint32_t* hist,
+                                          float& thr) {
+    return compact_query_body<CAP>(buf, n0, n1, k, hist, thr);
 }
 
 // Sort one query's buffer (halves of n0 / n1 entries, n0+n1 <= 64*E) and

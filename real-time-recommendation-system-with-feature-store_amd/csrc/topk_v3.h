@@ -1,6 +1,8 @@
-// Flat-IP top-K for 16-bit corpora with d <= 128 and k <= 128 — the C4 shape
-// (65,536 queries x a 125,000-row f16 shard, d = 128, k = 100). Included by
-// topk_impl.h; same contract, grid, plan and workspace as the v2 kernel
+// Flat-IP top-K for 16-bit corpora with d <= 128 and k <= RT_TOPK3_MAXK (32):
+// the small-k C4 shapes (65,536 queries x a 125,000-row f16 shard, d = 128,
+// k = 1 / 10); larger k goes to topk_v4.h (large corpora) or topk_v2.h (the
+// dispatch in topk_impl.h). Included by topk_impl.h; same contract, grid, plan
+// and workspace as the v2 kernel
 // (topk_v2.h), whose candidate buffers, radix compaction and final sort it
 // reuses. What differs is the scan, built for a low instruction count per
 // 32 x 32 score sub-tile (8 MFMAs at d = 128):

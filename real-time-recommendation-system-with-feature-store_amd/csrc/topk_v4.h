@@ -1,0 +1,768 @@
+// Flat-IP top-K for 16-bit corpora (f16 / bf16), d <= 128, k <= 128, on
+// large corpora — the C4 shape (65,536 queries x a 125,000-row shard, k = 100)
+// and the 1M-row corpus on one GPU. Included by topk_impl.h; replaces
+// faiss.IndexFlatIP.search (src/serving/retrieval.py:170-171) on that shape.
+//
+// Two launches:
+//
+// 1. flatip_topk_v4_scan: block = 8 waves x QS sets of 32 queries (QS = 2:
+//    64 queries per wave, 512 per block; every A fragment read from LDS feeds
+//    two MFMAs, and a block's item stream serves 512 queries), over one item
+//    split. Rows stream through the three-stage LDS ring of the v3 scan
+//    (SADDR LDS-DMA, one pad chunk per row, immediate-offset A fragments).
+//    Selection runs against a SAMPLED threshold instead of a running one:
+//      * sample phase: every `stride`-th stage of the split (a 1/stride
+//        sample). Per lane and query set the 16 largest group maxima
+//        (group = the 16 rows of a 32-row sub-tile a lane holds) are kept in
+//        a sorted register list, one v_med3 per level per insert, no ids.
+//      * the estimate: thr = the `rank`-th largest of the query's 32 group
+//        maxima (both lane halves). The host picks (stride, rank) so that
+//        P(thr > the split's k-th score) = P(Bin(k, 1/stride) >= rank) is
+//        below 1e-6 (topk_api.hip::plan_v4).
+//      * main phase: every stage (the sample stages again), each score >= thr
+//        appended to the query's candidate buffer (per lane half: one
+//        SADDR 8-byte store at the lane's cursor). About rank * stride
+//        appends per query (336 at k = 100), against thousands for a running
+//        threshold that starts at -inf. A half nearing its capacity is
+//        compacted by the v2 radix compaction (threshold raised, never lowered).
+//      * verification: a query whose buffer holds >= k entries (all >= thr)
+//        has its split top-k inside it, exactly. A query with fewer (the
+//        estimate overshot) makes the whole block rescan the split for its
+//        failed queries with thr = -inf and the compaction path of v2 —
+//        correct for any data, costly only when it happens.
+//    Each (split, query, half) writes its entry count to `meta`.
+// 2. flatip_topk_v4_finish: one wave per query over the union of its split
+//    buffers: a radix select on the composite key (order-preserving score
+//    key << 32 | ~id, larger = better: score desc, id asc) down to <= 1024
+//    survivors (usually k plus a few after 16 bits), one register bitonic
+//    sort, the k best written in Faiss order with (-FLT_MAX, -1) padding.
+//    The split merge is part of this pass (no topk_merge launch).
+#pragma once
+
+namespace rt {
+namespace topk {
+namespace v4 {
+
+constexpr int kWavesB = 8;
+constexpr int kCap = 1024;             // candidate entries per (split, query)
+constexpr int kHalf = kCap / 2;        // per owning lane half
+constexpr int kMaxK = 128;
+constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
+constexpr int kMaxSplits = 8;
+constexpr int kFinishCap = 1024;       // survivors a finish wave sorts at once
+
+template <int QS>
+struct Geo {
+    static constexpr int QT = 32 * QS * kWavesB;  // queries per block
+};
+
+template <typename T, int S>
+struct Cfg4 {
+    static_assert(sizeof(T) == 2 && S <= 8, "v4: 16-bit, d <= 128");
+    static constexpr int DP = S * 16;
+    static constexpr int P = DP * 2 / 16;          // 16-byte data chunks per row
+    static constexpr int RS = (P + 1) * 16;        // LDS row stride: one pad chunk
+    static constexpr int NT = 128;                 // rows per stage
+    static constexpr int NSUB = NT / 32;
+    static constexpr int SLOTS = NT * (P + 1);
+    static constexpr int PIECES = SLOTS / 64;      // 1 KiB DMA pieces per stage
+    static constexpr int MAXP = (PIECES + kWavesB - 1) / kWavesB;
+    static constexpr int TILE_BYTES = SLOTS * 16;
+    static constexpr int RING = 3;
+    static constexpr int SCR_BYTES = kWavesB * 64 * 80;   // per-lane score rows (80 B: conflict-free b128)
+    static constexpr int HIST_BYTES = kWavesB * 1024;
+    static constexpr int LDS_BYTES = RING * TILE_BYTES + SCR_BYTES + HIST_BYTES + 16;
+    static_assert(PIECES * 64 == SLOTS, "whole DMA pieces");
+    static_assert(LDS_BYTES <= 163840, "LDS budget");
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_exact() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <int LO, int HI>
+__device__ __forceinline__ void wait_vm_range(int n) {
+    if constexpr (LO == HI) {
+        wait_vm_exact<LO>();
+    } else {
+        constexpr int MID = (LO + HI) / 2;
+        if (n <= MID) wait_vm_range<LO, MID>(n);
+        else wait_vm_range<MID + 1, HI>(n);
+    }
+}
+// wait until at most n (wave-uniform) vector-memory operations are in flight
+__device__ __forceinline__ void wait_vm_le(int n) { wait_vm_range<0, 63>(n < 0 ? 0 : (n > 63 ? 63 : n)); }
+
+// sorted (descending) list insert without ids: l[i] <- med3(l[i], l[i-1], x)
+// (= clamp(x, l[i], l[i-1]) since l[i] <= l[i-1]) — one VALU per level
+__device__ __forceinline__ void list_insert_med3(float (&l)[kList], float x) {
+#pragma unroll
+    for (int i = kList - 1; i >= 1; --i) l[i] = __builtin_amdgcn_fmed3f(l[i], l[i - 1], x);
+    l[0] = fmaxf(l[0], x);
+}
+
+// the rank-th largest (1-based, rank <= 32) of the union of this lane's list
+// and its partner lane's (lane ^ 32); -inf when fewer finite entries exist
+__device__ __forceinline__ float union_rank(const float (&l)[kList], int rank) {
+    float u[2 * kList];
+#pragma unroll
+    for (int i = 0; i < kList; ++i) {
+        u[i] = l[i];
+        u[2 * kList - 1 - i] = __shfl_xor(l[i], 32, 64);  // partner's list ascending: u is bitonic
+    }
+#pragma unroll
+    for (int st = kList; st > 0; st >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 2 * kList; ++i) {
+            if ((i & st) == 0) {
+                const float a = u[i], b = u[i + st];
+                u[i] = fmaxf(a, b);
+                u[i + st] = fminf(a, b);
+            }
+        }
+    }
+    float v = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 2 * kList; ++i) v = (i == rank - 1) ? u[i] : v;
+    return v;
+}
+
+// composite key of a candidate: larger = better (score desc, then id asc)
+__device__ __forceinline__ uint64_t ckey(const Cand& c) {
+    return (static_cast<uint64_t>(v2::okey(c.s)) << 32) | static_cast<uint32_t>(~c.i);
+}
+__device__ __forceinline__ uint64_t prefix_mask(int shift) { return shift >= 64 ? 0ull : (~0ull << shift); }
+
+// Radix select over candidates visited by each(fn) (whole wave calls; fn gets
+// every entry exactly once, on some lane): 8 bits of the composite key a pass,
+// from the top, until the entries whose key's top (64 - shift) bits are >=
+// prefix's number <= limit. That set always holds the k best entries (k <=
+// limit). Registers: a few; LDS: hist (256 words, this wave's).
+template <class Each>
+__device__ __forceinline__ void radix_prefix(Each&& each, int k, int limit, uint32_t* hist, uint64_t& prefix,
+                                             int& shift, int& kept) {
+    const int lane = threadIdx.x & 63;
+    int need = k;  // entries still to be found inside the current prefix bucket
+    while (shift > 0) {
+        const int sh = shift - 8;
+        reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_sync();
+        const uint64_t pmask = prefix_mask(shift), pre = prefix;
+        each([&](const Cand& c) {
+            const uint64_t key = ckey(c);
+            if ((key & pmask) == pre) atomicAdd(&hist[(key >> sh) & 255u], 1u);
+        });
+        wave_lds_sync();
+        const uint4 h = reinterpret_cast<const uint4*>(hist)[lane];
+        const int c4 = static_cast<int>(h.x + h.y + h.z + h.w);
+        int suf = c4;  // inclusive suffix over lanes >= lane (bins ascend with lane)
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_down(suf, o, 64);
+            if (lane + o < 64) suf += t;
+        }
+        const int ab = suf - c4;
+        const int c3 = ab + static_cast<int>(h.w), c2 = c3 + static_cast<int>(h.z);
+        const int c1 = c2 + static_cast<int>(h.y), c0 = c1 + static_cast<int>(h.x);
+        const bool hit = ab < need && c0 >= need;
+        const uint64_t bm = __ballot(hit);
+        const int src = bm ? __builtin_ctzll(bm) : 0;
+        const int bl = c3 >= need ? 3 : c2 >= need ? 2 : c1 >= need ? 1 : 0;
+        const int al = c3 >= need ? ab : c2 >= need ? c3 : c1 >= need ? c2 : c1;
+        const int inb = c3 >= need   ? static_cast<int>(h.w)
+                        : c2 >= need ? static_cast<int>(h.z)
+                        : c1 >= need ? static_cast<int>(h.y)
+                                     : static_cast<int>(h.x);
+        const int bin = __shfl(4 * lane + bl, src, 64);
+        const int above = __shfl(al, src, 64);
+        const int inbin = __shfl(inb, src, 64);
+        wave_lds_sync();
+        prefix |= static_cast<uint64_t>(bin) << sh;
+        shift = sh;
+        need -= above;
+        kept = (k - need) + inbin;  // strictly above the bucket + the bucket
+        if (kept <= limit) break;
+    }
+}
+
+// In-scan compaction of one query's buffer (halves of n0 / n1 entries, k <=
+// n0 + n1), streamed from memory so that the scan keeps its registers: each
+// half keeps, in place and in order, its entries in the radix bucket holding
+// the k best (<= limit entries in all). thr = the new filter threshold:
+// the bucket's score floor (v >= thr), or, when the bucket had to be resolved
+// down into the ids (massive exact ties), strictly above the k-th score — items
+// arrive in increasing id order, so an equal later score loses.
+__device__ __forceinline__ void compact_stream(Cand* __restrict__ buf, int& n0, int& n1, int k, int limit,
+                                               uint32_t* hist, float& thr) {
+    const int lane = threadIdx.x & 63;
+    __threadfence_block();
+    const int a0 = n0, a1 = n1;
+    auto each = [&](auto&& fn) {
+        for (int i = lane; i < a0; i += 64) fn(buf[i]);
+        for (int i = lane; i < a1; i += 64) fn(buf[kHalf + i]);
+    };
+    uint64_t prefix = 0;
+    int shift = 64, kept = a0 + a1;
+    radix_prefix(each, k, limit, hist, prefix, shift, kept);
+    const uint64_t pmask = prefix_mask(shift);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Cand* p = buf + h * kHalf;
+        const int n = h ? a1 : a0;
+        int m = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            Cand c{-INFINITY, kEmptyId};
+            bool take = false;
+            if (i < n) {
+                c = p[i];
+                take = (ckey(c) & pmask) >= prefix;
+            }
+            const uint64_t bm = __ballot(take);
+            const int pos = m + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                    static_cast<uint32_t>(bm >> 32),
+                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bm), 0u)));
+            if (take) p[pos] = c;  // pos <= i: every lane read its entry before any lane writes
+            m += __popcll(bm);
+        }
+        if (h) n1 = m;
+        else n0 = m;
+    }
+    const float floor = v2::okey_inv(static_cast<uint32_t>(prefix >> 32));
+    if (shift >= 32) thr = (static_cast<uint32_t>(prefix >> 32) <= 0x007FFFFFu) ? -FLT_MAX : floor;
+    else thr = nextafterf(floor, INFINITY);
+    __threadfence_block();
+}
+
+template <typename T, int S, int QS, bool EXCL>
+__global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, int64_t items_per_split, int stride,
+                                                            int rank, int* __restrict__ meta) {
+    using M = Mfma<T>;
+    using C = Cfg4<T, S>;
+    typedef typename M::frag frag;
+    constexpr int QT = Geo<QS>::QT;
+    __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
+    char* const ring = lds;
+    float* const scr = reinterpret_cast<float*>(lds + C::RING * C::TILE_BYTES);
+    uint32_t* const hist_all = reinterpret_cast<uint32_t*>(lds + C::RING * C::TILE_BYTES + C::SCR_BYTES);
+    uint32_t* const flag = hist_all + kWavesB * 256;
+
+    const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
+    const char* __restrict__ Xb = reinterpret_cast<const char*>(a.X);
+    const int d = a.d, k = a.k;
+    const int64_t nq = a.nq;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, col = lane & 31, half = lane >> 5;
+    const int split = static_cast<int>(blockIdx.x % static_cast<unsigned>(splits));
+    const int64_t qtile = blockIdx.x / static_cast<unsigned>(splits);
+    const int64_t qw = qtile * QT + wave * (32 * QS);  // wave's first query
+    const int64_t i_begin = static_cast<int64_t>(split) * items_per_split;
+    const int64_t i_end = (i_begin + items_per_split) < a.nx ? (i_begin + items_per_split) : a.nx;
+    const int64_t row_bytes = static_cast<int64_t>(d) * 2;
+    const int64_t q_pad = static_cast<int64_t>(gridDim.x / splits) * QT;
+    Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32·QS buffers
+    uint32_t* const whist = hist_all + wave * 256;
+    float* const wscr = scr + (wave * 64 + lane) * 20;
+    const int nst = i_end > i_begin ? static_cast<int>((i_end - i_begin + C::NT - 1) / C::NT) : 0;
+    const int nsa = (rank > 0 && stride > 0) ? (nst + stride - 1) / stride : 0;  // sample stages
+    if (tid == 0) *flag = 0u;
+
+    frag qf[QS][S];
+    bool qok[QS];
+    const uint32_t* excl[QS];
+#pragma unroll
+    for (int j = 0; j < QS; ++j) {
+        const int64_t q = qw + j * 32 + col;
+        qok[j] = q < nq;
+        const T* qrow = Q + (qok[j] ? q : 0) * d;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int k0 = 16 * s + 8 * half;
+            if (qok[j] && k0 < d) qf[j][s] = frag_from<T>(qrow + k0);
+            else qf[j][s] = frag{};
+        }
+        excl[j] = (EXCL && qok[j]) ? a.excl + q * a.excl_words : nullptr;
+    }
+#pragma unroll
+    for (int j = 0; j < QS; ++j)
+#pragma unroll
+        for (int s = 0; s < S; ++s) {  // drained here, not at the loop header's merged wait
+            const uint4 t = __builtin_bit_cast(uint4, qf[j][s]);
+            asm volatile("" ::"v"(t.x), "v"(t.y), "v"(t.z), "v"(t.w));
+        }
+
+    // ---- append cursors: byte offset of the lane's next entry from the wave's base ----
+    const uint32_t wb_lo = static_cast<uint32_t>(
+        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase))));
+    const uint32_t wb_hi = static_cast<uint32_t>(
+        __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase) >> 32)));
+    const uint64_t wbase = (static_cast<uint64_t>(wb_hi) << 32) | wb_lo;
+    uint32_t woff0[QS], woff[QS];
+    float thr[QS];
+#pragma unroll
+    for (int j = 0; j < QS; ++j) {
+        woff0[j] = static_cast<uint32_t>(((j * 32 + col) * kCap + half * kHalf) * sizeof(Cand));
+        woff[j] = woff0[j];
+        thr[j] = qok[j] ? -FLT_MAX : INFINITY;
+    }
+    constexpr int kHead = C::NSUB * 16;  // appends per half between two compaction checks, at most
+    constexpr uint32_t kLimBytes = static_cast<uint32_t>((kHalf - kHead) * sizeof(Cand));
+    constexpr int kLimit = kHalf - kHead;  // a compaction keeps at most this many entries (in all)
+
+    // ---- DMA plan (as v3): this wave's pieces w, w+8, ... of a stage ----
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    const int npieces = (C::PIECES - wave_u + kWavesB - 1) / kWavesB;
+    const int row_vecs = d / 8;
+    uint32_t soff[C::MAXP];
+#pragma unroll
+    for (int i = 0; i < C::MAXP; ++i) {
+        const int o = (wave_u + kWavesB * i) * 64 + lane;
+        const int r = o / (C::P + 1), c = o % (C::P + 1);
+        soff[i] = static_cast<uint32_t>(r * static_cast<int>(row_bytes) + (c < row_vecs ? c * 16 : 0));
+    }
+    const uint32_t ring0 = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) char*)(ring)));
+    int issued = 0;
+    int mk[C::RING - 1];
+    auto fetch = [&](int64_t t0, int buf) {
+        const uint32_t base = ring0 + buf * C::TILE_BYTES + wave_u * 1024;
+        const uint64_t sbu = reinterpret_cast<uint64_t>(Xb + t0 * row_bytes);
+        const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);
+#pragma unroll
+        for (int i = 0; i < C::MAXP; ++i) {
+            if (i < npieces) {
+                uint32_t off = soff[i];
+                if (rem < C::NT) {  // rows past the split end read its last row (masked)
+                    const int r = ((wave_u + kWavesB * i) * 64 + lane) / (C::P + 1);
+                    if (r >= rem) off -= static_cast<uint32_t>((r - (rem - 1)) * row_bytes);
+                }
+                unsigned keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                    "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "v"(off), "s"(sbu), "s"(base + i * (kWavesB * 1024))
+                    : "memory");
+            }
+        }
+        issued += npieces;
+    };
+    auto raw_barrier = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    // ---- selection (per query set j) ----
+    auto max16 = [&](const f32x16& acc) {
+        float m = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) m = fmaxf(fmaxf(m, acc[r]), acc[r + 1]);
+        return fmaxf(m, acc[15]);
+    };
+    auto appends = [&](int j, const f32x16& acc, int64_t sub0, float m) {
+        if (__ballot(m >= thr[j]) == 0) return;
+        uint32_t bits = 0u;  // bit 15-r <=> acc[r] passes
+        const float t = thr[j];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            asm("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
+                : "+v"(bits)
+                : "v"(acc[r]), "v"(t)
+                : "vcc");
+        if constexpr (EXCL) {
+            if (excl[j]) {
+                const uint32_t xw = excl[j][sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if ((xw >> tile_row(r, half)) & 1u) bits &= ~(1u << (15 - r));
+            }
+        }
+        if (bits) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<float4*>(wscr + 4 * i) =
+                    make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        }
+        const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
+        uint32_t wo = woff[j];
+        while (__ballot(bits != 0u)) {
+            issued += 2;  // exactly two store instructions for the wave
+            if (bits) {
+                const int b = 31 - __builtin_clz(bits);  // highest set bit = lowest r
+                bits &= ~(1u << b);
+                const int r = 15 - b;
+                const float v = wscr[r];  // same-wave LDS write → read: in order
+                const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
+                asm volatile(
+                    "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
+                    "v_add_u32 %0, 8, %0"
+                    : "+v"(wo)
+                    : "v"(v), "s"(wbase), "v"(id)
+                    : "memory");
+            }
+        }
+        woff[j] = wo;
+    };
+    // compact every buffer of this wave that may overflow before the next check
+    auto maybe_compact = [&]() {
+#pragma unroll
+        for (int j = 0; j < QS; ++j) {
+            const uint64_t m = __ballot(woff[j] - woff0[j] > kLimBytes);
+            uint32_t need = static_cast<uint32_t>(m) | static_cast<uint32_t>(m >> 32);
+            if (!need) continue;
+            while (need) {
+                const int c = __builtin_ctz(need);
+                need &= need - 1;
+                const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
+                int n0 = __shfl(cnt, c, 64), n1 = __shfl(cnt, c + 32, 64);
+                float nt;
+                compact_stream(cbase + static_cast<int64_t>(j * 32 + c) * kCap, n0, n1, k, kLimit, whist, nt);
+                if (col == c) {
+                    woff[j] = woff0[j] + static_cast<uint32_t>((half ? n1 : n0) * sizeof(Cand));
+                    thr[j] = fmaxf(thr[j], nt);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < C::RING - 1; ++i) mk[i] = issued;  // drained
+        }
+    };
+
+    // ---- MFMA sub-tiles ----
+    const int a_lane = col * C::RS + half * 16;
+    auto lds_a = [&](frag (&af)[S], const char* stage, int rt) {
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            af[s] = __builtin_bit_cast(frag, *reinterpret_cast<const uint4*>(stage + rt * 32 * C::RS + s * 32));
+    };
+    auto mask_tail = [&](f32x16& acc, int64_t sub0) {
+        const int left = static_cast<int>(i_end - sub0);
+        if (left < 32) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (tile_row(r, half) >= left) acc[r] = -INFINITY;
+        }
+    };
+    auto mask_excl = [&](int j, f32x16& acc, int64_t sub0) {
+        if constexpr (EXCL) {
+            if (excl[j]) {
+                const uint32_t xw = excl[j][sub0 >> 5];
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if ((xw >> tile_row(r, half)) & 1u) acc[r] = -INFINITY;
+            }
+        }
+    };
+
+    // stage v of a pass: rows [stage_row(v), +NT); `sample` passes visit every
+    // stride-th stage
+    auto stage_t0 = [&](int v, bool sample) -> int64_t {
+        return i_begin + static_cast<int64_t>(sample ? v * stride : v) * C::NT;
+    };
+
+    // ---- sample pass: group-max lists ----
+    float L[QS][kList];
+#pragma unroll
+    for (int j = 0; j < QS; ++j)
+#pragma unroll
+        for (int i = 0; i < kList; ++i) L[j][i] = -INFINITY;
+
+    auto prologue = [&](int nv, bool sample) {
+        int mark0 = 0;
+#pragma unroll
+        for (int b = 0; b < C::RING - 1; ++b) {
+            if (b < nv) fetch(stage_t0(b, sample), b);
+            if (b == 0) mark0 = issued;
+            else mk[b - 1] = issued;
+        }
+        wait_vm_le(issued - mark0);
+        raw_barrier();
+    };
+
+    if (nsa > 0) {
+        prologue(nsa, true);
+        int cur = 0;
+        for (int v = 0; v < nsa; ++v) {
+            const int64_t t0 = stage_t0(v, true);
+            const bool more = v + 1 < nsa;
+            const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);
+            if (v + C::RING - 1 < nsa) fetch(stage_t0(v + C::RING - 1, true), cur == 0 ? C::RING - 1 : cur - 1);
+            mk[C::RING - 2] = issued;
+            const char* stage = ring + cur * C::TILE_BYTES + a_lane;
+#pragma unroll
+            for (int rt = 0; rt < C::NSUB; ++rt) {
+                if (rt * 32 < rem) {
+                    frag af[S];
+                    lds_a(af, stage, rt);
+                    f32x16 acc[QS];
+#pragma unroll
+                    for (int j = 0; j < QS; ++j) {
+                        acc[j] = f32x16{};
+#pragma unroll
+                        for (int s = 0; s < S; ++s) acc[j] = M::run(af[s], qf[j][s], acc[j]);
+                    }
+                    const int64_t sub0 = t0 + rt * 32;
+#pragma unroll
+                    for (int j = 0; j < QS; ++j) {
+                        if (rem < (rt + 1) * 32) mask_tail(acc[j], sub0);
+                        mask_excl(j, acc[j], sub0);
+                        list_insert_med3(L[j], max16(acc[j]));
+                    }
+                }
+            }
+            if (more) wait_vm_le(issued - mk[0]);
+            raw_barrier();
+#pragma unroll
+            for (int i = 0; i + 1 < C::RING - 1; ++i) mk[i] = mk[i + 1];
+            cur = cur == C::RING - 1 ? 0 : cur + 1;
+        }
+#pragma unroll
+        for (int j = 0; j < QS; ++j) {
+            const float e = union_rank(L[j], rank);
+            if (qok[j]) thr[j] = e > -FLT_MAX ? e : -FLT_MAX;
+        }
+    }
+
+    // ---- main pass over every stage (A fragments of sub-tile t+1 read behind t's MFMAs;
+    //      set QS-1 of sub-tile t is filtered during set 0's MFMAs of t+1) ----
+    auto main_pass = [&]() {
+        if (nst == 0) return;
+        prologue(nst, false);
+        frag af[S];
+        f32x16 acc[QS];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[QS - 1][r] = -INFINITY;  // "previous" of the first sub-tile
+        int64_t sub_prev = i_begin;
+        int cur = 0;
+        lds_a(af, ring + a_lane, 0);
+        for (int v = 0; v < nst; ++v) {
+            const int64_t t0 = stage_t0(v, false);
+            const bool more = v + 1 < nst;
+            const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);
+            if (v + C::RING - 1 < nst) fetch(stage_t0(v + C::RING - 1, false), cur == 0 ? C::RING - 1 : cur - 1);
+            mk[C::RING - 2] = issued;
+            const char* stage = ring + cur * C::TILE_BYTES + a_lane;
+#pragma unroll
+            for (int rt = 0; rt < C::NSUB; ++rt) {
+                if (rt * 32 < rem) {
+                    const int64_t sub0 = t0 + rt * 32;
+                    const bool next_here = rt + 1 < C::NSUB && (rt + 1) * 32 < rem;
+                    // set 0: MFMAs, with the previous sub-tile's last set reduced in the gaps
+                    float mp = 0.f;
+                    acc[0] = f32x16{};
+#pragma unroll
+                    for (int s = 0; s < S; ++s) {
+                        acc[0] = M::run(af[s], qf[0][s], acc[0]);
+                        if constexpr (QS > 1) {
+                            const f32x16& p = acc[QS - 1];
+                            if (s == 0) mp = fmaxf(fmaxf(p[0], p[1]), p[2]);
+                            if (s == 1) mp = fmaxf(fmaxf(mp, p[3]), p[4]);
+                            if (s == 2) mp = fmaxf(fmaxf(mp, p[5]), p[6]);
+                            if (s == 3) mp = fmaxf(fmaxf(mp, p[7]), p[8]);
+                            if (s == 4 || (S < 8 && s == S - 1)) {
+                                mp = fmaxf(fmaxf(mp, p[9]), p[10]);
+                                mp = fmaxf(fmaxf(mp, p[11]), p[12]);
+                                mp = fmaxf(fmaxf(mp, p[13]), p[14]);
+                                mp = fmaxf(mp, p[15]);
+                            }
+                        }
+                    }
+                    if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev, mp);
+                    if (rem < (rt + 1) * 32) mask_tail(acc[0], sub0);
+                    if constexpr (QS == 1) {
+                        if (next_here) lds_a(af, stage, rt + 1);
+                    }
+#pragma unroll
+                    for (int j = 1; j < QS; ++j) {
+                        float m0 = 0.f;
+                        acc[j] = f32x16{};
+#pragma unroll
+                        for (int s = 0; s < S; ++s) {
+                            acc[j] = M::run(af[s], qf[j][s], acc[j]);
+                            if (j == QS - 1 && next_here)  // fragment s is free once its last MFMA issued
+                                af[s] = __builtin_bit_cast(
+                                    frag, *reinterpret_cast<const uint4*>(stage + (rt + 1) * 32 * C::RS + s * 32));
+                            const f32x16& p = acc[j - 1];
+                            if (s == 0) m0 = fmaxf(fmaxf(p[0], p[1]), p[2]);
+                            if (s == 1) m0 = fmaxf(fmaxf(m0, p[3]), p[4]);
+                            if (s == 2) m0 = fmaxf(fmaxf(m0, p[5]), p[6]);
+                            if (s == 3) m0 = fmaxf(fmaxf(m0, p[7]), p[8]);
+                            if (s == 4 || (S < 8 && s == S - 1)) {
+                                m0 = fmaxf(fmaxf(m0, p[9]), p[10]);
+                                m0 = fmaxf(fmaxf(m0, p[11]), p[12]);
+                                m0 = fmaxf(fmaxf(m0, p[13]), p[14]);
+                                m0 = fmaxf(m0, p[15]);
+                            }
+                        }
+                        appends(j - 1, acc[j - 1], sub0, m0);
+                        if (rem < (rt + 1) * 32) mask_tail(acc[j], sub0);
+                    }
+                    if constexpr (QS == 1) appends(0, acc[0], sub0, max16(acc[0]));
+                    sub_prev = sub0;
+                }
+            }
+            if (more) wait_vm_le(issued - mk[0]);
+            raw_barrier();
+#pragma unroll
+            for (int i = 0; i + 1 < C::RING - 1; ++i) mk[i] = mk[i + 1];
+            cur = cur == C::RING - 1 ? 0 : cur + 1;
+            if (more) {
+                maybe_compact();  // the only check in the loop: between stages, before any fragment is live
+                lds_a(af, ring + cur * C::TILE_BYTES + a_lane, 0);
+            }
+        }
+        if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev, max16(acc[QS - 1]));
+        maybe_compact();
+    };
+    main_pass();
+
+    // ---- verification: a sampled threshold that left < k entries rescans ----
+    if (nsa > 0) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < QS; ++j) {
+            const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
+            const int tot = cnt + __shfl_xor(cnt, 32, 64);
+            const bool fail = qok[j] && tot < k;
+            any |= fail;
+            if (fail) {
+                thr[j] = -FLT_MAX;  // start over for this query: empty buffer, v2 selection
+                woff[j] = woff0[j];
+            } else {
+                thr[j] = INFINITY;  // done: no appends in the rescan
+            }
+        }
+        if (__ballot(any) != 0 && lane == 0) atomicOr(flag, 1u);
+        __syncthreads();
+        if (*flag) main_pass();  // block-uniform
+    }
+
+    // ---- entry counts for the finish pass ----
+#pragma unroll
+    for (int j = 0; j < QS; ++j) {
+        const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
+        meta[((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * 2 + half] = cnt;
+    }
+}
+
+// ---- finish: radix select over the union of a query's split buffers ----
+
+template <int E>
+__device__ __noinline__ void finish_sort(const Cand* __restrict__ buf, int m, int k, float* __restrict__ os,
+                                         int64_t* __restrict__ oi, int64_t id_offset) {
+    const int lane = threadIdx.x & 63;
+    float s[E];
+    uint32_t id[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const int r = lane * E + j;
+        const Cand c = r < m ? buf[r] : Cand{-INFINITY, kEmptyId};
+        s[j] = c.s;
+        id[j] = c.i;
+    }
+    wave_sort_regs<E>(s, id);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const int r = lane * E + j;
+        if (r < k) {
+            const bool ok = id[j] != kEmptyId;
+            os[r] = ok ? s[j] : -FLT_MAX;
+            oi[r] = ok ? static_cast<int64_t>(id[j]) + id_offset : -1;
+        }
+    }
+}
+
+// one wave per query; block = 4 waves (a template only so that the three
+// per-dtype translation units that include this header share one definition)
+template <int NW = 4>
+__global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restrict__ cand,
+                                                             const int* __restrict__ meta, int splits,
+                                                             int64_t q_pad, int64_t nq, int k,
+                                                             float* __restrict__ out_s, int64_t* __restrict__ out_i,
+                                                             int64_t id_offset) {
+    __shared__ __attribute__((aligned(16))) uint32_t hist_all[4][256];
+    __shared__ __attribute__((aligned(16))) Cand keep_all[4][kFinishCap];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + w;
+    if (q >= nq) return;
+    uint32_t* hist = hist_all[w];
+    Cand* keep = keep_all[w];
+    const int nseg = 2 * splits;
+    // segment (split s, half h) = lane 2s+h: entry count and exclusive prefix
+    int cnt = 0;
+    if (lane < nseg) cnt = meta[((static_cast<int64_t>(lane >> 1) * q_pad) + q) * 2 + (lane & 1)];
+    int pre = cnt;  // inclusive prefix over lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(pre, o, 64);
+        if (lane >= o) pre += t;
+    }
+    const int total = __shfl(pre, 63, 64);
+    auto seg_ptr = [&](int sg) {
+        return cand + ((static_cast<int64_t>(sg >> 1) * q_pad) + q) * kCap + (sg & 1) * kHalf;
+    };
+    // visit every entry: fn(entry); segments in order, lanes strided
+    auto each = [&](auto&& fn) {
+        for (int sg = 0; sg < nseg; ++sg) {
+            const int n = __shfl(cnt, sg, 64);
+            const Cand* p = seg_ptr(sg);
+            for (int i = lane; i < n; i += 64) fn(p[i]);
+        }
+    };
+    float* os = out_s + q * k;
+    int64_t* oi = out_i + q * k;
+
+    // radix select on the composite key until <= kFinishCap entries remain
+    uint64_t prefix = 0;
+    int shift = 64, kept = total;
+    if (total > kFinishCap) radix_prefix(each, k, kFinishCap, hist, prefix, shift, kept);
+    // collect entries with key >= prefix (lower bits zero) into LDS, in any order
+    const uint64_t pmask = prefix_mask(shift);
+    int m = 0;
+    for (int sg = 0; sg < nseg; ++sg) {
+        const int n = __shfl(cnt, sg, 64);
+        const Cand* p = seg_ptr(sg);
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            Cand c{-INFINITY, kEmptyId};
+            bool take = false;
+            if (i < n) {
+                c = p[i];
+                take = (ckey(c) & pmask) >= prefix;
+            }
+            const uint64_t bm = __ballot(take);
+            const int pos = m + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                    static_cast<uint32_t>(bm >> 32),
+                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bm), 0u)));
+            if (take && pos < kFinishCap) keep[pos] = c;
+            m += __popcll(bm);
+        }
+    }
+    if (m > kFinishCap) m = kFinishCap;  // cannot happen: the prefix bounds it
+    wave_lds_sync();
+    if (m <= 128) finish_sort<2>(keep, m, k, os, oi, id_offset);
+    else if (m <= 256) finish_sort<4>(keep, m, k, os, oi, id_offset);
+    else if (m <= 512) finish_sort<8>(keep, m, k, os, oi, id_offset);
+    else finish_sort<16>(keep, m, k, os, oi, id_offset);
+}
+
+template <typename T, int S, int QS>
+int launch_S(const Args& a, int q_tiles, int splits, int64_t items_per_split, int stride, int rank, int* meta,
+             hipStream_t st) {
+    dim3 grid(static_cast<unsigned>(q_tiles * splits));
+    if (a.excl)
+        hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, true>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                           items_per_split, stride, rank, meta);
+    else
+        hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, false>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                           items_per_split, stride, rank, meta);
+    int rc = check_launch("flatip_topk_v4_scan");
+    if (rc) return rc;
+    const int64_t q_pad = static_cast<int64_t>(q_tiles) * Geo<QS>::QT;
+    hipLaunchKernelGGL(flatip_topk_v4_finish<4>, dim3(static_cast<unsigned>((a.nq + 3) / 4)), dim3(256), 0, st, a.cand,
+                       meta, splits, q_pad, a.nq, a.k, a.out_s, a.out_i, a.id_offset);
+    return check_launch("flatip_topk_v4_finish");
+}
+
+}  // namespace v4
+}  // namespace topk
+}  // namespace rt

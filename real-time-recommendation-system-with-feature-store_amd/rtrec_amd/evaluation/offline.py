@@ -14,8 +14,14 @@ orders exact score ties by a quicksort-dependent rule; outside exact ties the
 lists are identical (tests/test_gpu_eval.py checks this tie-aware against the
 reference's own output, tests/golden/eval_topk.npz). When a user has fewer
 than ``top_k`` non-train items the reference appends its ``-inf`` train items
-in argsort order; this build returns only the eligible items (the reference's
-Evaluator removes those train items again before scoring, metrics.py:279-281).
+in argsort order; by default this build returns only the eligible items (the
+reference's Evaluator removes those train items again before scoring,
+metrics.py:279-281). ``pad_excluded=True`` returns the reference's full-length
+lists instead: such a user's top_k already holds every eligible item with its
+score, so the masked score row is known exactly, and the list is
+``np.argsort(row)[::-1][:top_k]`` over it — the reference's own call
+(evaluate_model.py:225-231), whose order among the ``-inf`` ties is numpy's
+(its introsort/SIMD sort is not stable, so no other rule reproduces it).
 
 ``load_model`` (evaluate_model.py:36-95): architecture inferred from the
 checkpoint's weight shapes, ``weights_only=True``.
@@ -60,12 +66,24 @@ def recommend_tensors(model: TwoTowerModel, user_features: torch.Tensor, item_fe
     return kernels.flatip_topk(user_emb.contiguous(), item_emb.contiguous(), top_k, exclude_bits=bits)
 
 
+def _pad_like_reference(ids_row: np.ndarray, scores_row: np.ndarray, n_items: int, top_k: int) -> List[int]:
+    """A user with fewer than top_k eligible items: rebuild the reference's masked
+    score row (eligible items' scores, -inf elsewhere) and take its argsort,
+    as scripts/evaluate_model.py:225-231 does."""
+    ok = ids_row >= 0
+    row = np.full(n_items, -np.inf, dtype=np.float32)
+    row[ids_row[ok]] = scores_row[ok]
+    return [int(x) for x in np.argsort(row)[::-1][:top_k]]
+
+
 def generate_recommendations(model: TwoTowerModel, test_users: list, train_items: Dict[int, list],
                              user_features: np.ndarray, movie_features: np.ndarray, top_k: int = 100,
                              batch_size: int = 256, device: Optional[str] = None,
-                             return_tensors: bool = False):
+                             return_tensors: bool = False, pad_excluded: bool = False):
     """evaluate_model.py:162-234 → Dict[user_idx, List[movie_idx]] (or the
-    device (scores, ids) with ``return_tensors``)."""
+    device (scores, ids) with ``return_tensors``). ``pad_excluded``: lists of
+    users with fewer than ``top_k`` eligible items are padded with their
+    excluded items as the reference pads them (see the module docstring)."""
     dev = _dev(device)
     uf = torch.as_tensor(np.asarray(user_features, np.float32)).to(dev)
     mf = torch.as_tensor(np.asarray(movie_features, np.float32)).to(dev)
@@ -81,7 +99,17 @@ def generate_recommendations(model: TwoTowerModel, test_users: list, train_items
     if return_tensors:
         return scores, ids
     host = ids.cpu().numpy()
-    return {u: [int(x) for x in host[r] if x >= 0] for r, u in enumerate(users)}
+    if not pad_excluded:
+        return {u: [int(x) for x in host[r] if x >= 0] for r, u in enumerate(users)}
+    n_items = mf.shape[0]
+    host_s = scores.cpu().numpy()
+    out = {}
+    for r, u in enumerate(users):
+        if top_k <= n_items and (host[r] < 0).any():
+            out[u] = _pad_like_reference(host[r], host_s[r], n_items, top_k)
+        else:
+            out[u] = [int(x) for x in host[r] if x >= 0]
+    return out
 
 
 def load_model(checkpoint_path: str, user_dim: int, item_dim: int, device: Optional[str] = None) -> TwoTowerModel:

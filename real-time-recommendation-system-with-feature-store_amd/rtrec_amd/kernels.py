@@ -125,6 +125,14 @@ def flatip_topk(queries: torch.Tensor, items: torch.Tensor, k: int,
     return scores, ids
 
 
+def topk_tuning(v4_mode: int = 0, v4_stride: int = 0, v4_rank: int = -1) -> None:
+    """Planner override of flatip_topk (rt_flatip_topk_tuning; process-wide,
+    results unchanged): v4_mode 0 automatic / 1 never / 2 wherever legal the
+    sampled-threshold kernel pair; v4_stride the sample stride in 128-row stages
+    (0 = planner); v4_rank the sampled rank (-1 = planner, 0 = no sample)."""
+    call("rt_flatip_topk_tuning", int(v4_mode), int(v4_stride), int(v4_rank))
+
+
 def l2_augment(x: torch.Tensor, role: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """[n, d] fp32 → [n, d+4] augmented rows for the L2 mode (rt_l2_augment_f32):
     role 0 (queries) appends 1, role 1 (items) appends -||x||^2/2."""
@@ -143,11 +151,19 @@ def flatl2_topk(q_aug: torch.Tensor, x_aug: torch.Tensor, d: int, k: int,
                 exclude_bits: Optional[torch.Tensor] = None, id_offset: int = 0
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact squared-L2 k-NN on augmented rows (IndexFlatL2.search): (distances
-    [nq, k] ascending, ids [nq, k]); unfilled slots (FLT_MAX, -1)."""
-    s, i = flatip_topk(q_aug, x_aug, k, exclude_bits=exclude_bits, id_offset=id_offset)
-    call("rt_l2_finish_f32", ptr(q_aug), q_aug.shape[1], ptr(x_aug), x_aug.shape[1], d, q_aug.shape[0], k, ptr(s),
-         ptr(i), id_offset, stream_of(q_aug))
+    [nq, k] ascending, ids [nq, k]); unfilled slots (FLT_MAX, -1). k + 32
+    candidates are selected on the augmented inner product and re-ranked on
+    Faiss's distance (rt_l2_finish_f32)."""
+    k_sel = min(k + L2_MARGIN, 512)
+    _, sel = flatip_topk(q_aug, x_aug, k_sel, exclude_bits=exclude_bits, id_offset=id_offset)
+    s = torch.empty((q_aug.shape[0], k), dtype=torch.float32, device=q_aug.device)
+    i = torch.empty((q_aug.shape[0], k), dtype=torch.int64, device=q_aug.device)
+    call("rt_l2_finish_f32", ptr(q_aug), q_aug.shape[1], ptr(x_aug), x_aug.shape[1], d, q_aug.shape[0], k_sel,
+         ptr(sel), k, ptr(s), ptr(i), id_offset, stream_of(q_aug))
     return s, i
+
+
+L2_MARGIN = 32  # over-selected candidates per query in the L2 mode
 
 
 def topk_merge(scores: torch.Tensor, ids: torch.Tensor, k_out: int

@@ -59,6 +59,15 @@ def test_trainer_resumes_reference_checkpoint(device, golden, tmp_path):
     assert epoch == 1
     np.testing.assert_allclose(tr.train_losses, g["losses"][:1], rtol=1e-12)
     assert int(tr.step.step_dev.item()) == 1
+    # the loaded Adam state is the reference optimizer's, bit for bit, in its
+    # parameter order (a swapped mapping or a biased step count fails here)
+    ref_ck = torch.load(GOLDEN / "ckpt_ref_trainer.pth", map_location="cpu", weights_only=True)
+    mine = tr.step.optimizer_state_dict()["state"]
+    assert set(mine) == set(ref_ck["optimizer_state"]["state"])
+    for i, st in ref_ck["optimizer_state"]["state"].items():
+        assert torch.equal(mine[i]["exp_avg"], st["exp_avg"]), i
+        assert torch.equal(mine[i]["exp_avg_sq"], st["exp_avg_sq"]), i
+        assert float(mine[i]["step"]) == float(st["step"])
     batch = {k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("b1_")}
     tr.train_loader = [batch]
     loss = tr.train_epoch(2)
@@ -74,10 +83,20 @@ def test_trainer_resumes_reference_checkpoint(device, golden, tmp_path):
             # second Adam step from identical moments: ~lr-sized moves, tight elsewhere
             assert np.mean(diff <= 1e-5 + 1e-4 * np.abs(ref)) > 0.995, (k, diff.max())
             assert diff.max() <= 1.1e-3, (k, diff.max())
+    # the moments after that step against the reference optimizer's own
+    # (tests/golden/ckpt_ref_moments.npz): tight, since both start from the
+    # same state and differ only by the fp32 gradient rounding
+    mo = golden("ckpt_ref_moments")
+    after = tr.step.optimizer_state_dict()["state"]
+    for i, st in after.items():
+        assert float(st["step"]) == float(mo[f"step/{i}"]) == 2.0
+        for name in ("exp_avg", "exp_avg_sq"):
+            ref = mo[f"{name}/{i}"]
+            np.testing.assert_allclose(st[name].numpy(), ref, rtol=1e-4, atol=1e-6 * float(np.abs(ref).max() + 1e-30),
+                                       err_msg=f"{name}/{i}")
     # and what we write reads back in the same layout (our save -> our resume)
     tr.save_checkpoint(2, is_best=True)
     ck = torch.load(tmp_path / "two_tower_best.pth", map_location="cpu", weights_only=True)
-    ref_ck = torch.load(GOLDEN / "ckpt_ref_trainer.pth", map_location="cpu", weights_only=True)
     assert set(ck) == set(ref_ck)
     assert set(ck["optimizer_state"]["state"]) == set(ref_ck["optimizer_state"]["state"])
     assert ck["epoch"] == 2

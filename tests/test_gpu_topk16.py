@@ -120,3 +120,50 @@ def test_topk16_c4_shard_properties(K, k):
     rs, ri = orc.flat_ip_search(np.ascontiguousarray(qs), x.float().cpu().numpy(), k, nthreads=16)
     assert np.array_equal(gi.cpu().numpy()[sel], ri)
     assert np.array_equal(gs.cpu().numpy()[sel], rs)
+
+
+# ---- the sampled-threshold kernel pair (csrc/topk_v4.h) --------------------
+@pytest.fixture
+def V4(K):
+    """Force the v4 scan + finish pair on shapes the planner would give to
+    v2/v3 (small corpora, any k <= 128), with the given sample; restored after."""
+    def set_(stride=0, rank=-1, mode=2):
+        K.topk_tuning(mode, stride, rank)
+    yield set_
+    K.topk_tuning(0, 0, -1)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("nq,nx,d,k", [(700, 40000, 128, 100), (300, 20000, 64, 40), (129, 30011, 128, 128),
+                                       (600, 25000, 96, 10), (64, 9000, 128, 1)])
+def test_topk16_v4_dyadic_bit_exact(K, V4, dtype, nq, nx, d, k):
+    """Planner's (stride, rank) for the split; several splits merged by the
+    finish pass; ragged last stage (nx not a multiple of 128)."""
+    V4()
+    rng = np.random.default_rng(nq + nx + d + k)
+    _check(K, _dyadic(rng, nq, d), _dyadic(rng, nx, d), k, dtype)
+
+
+@pytest.mark.parametrize("stride,rank", [(4, 1), (32, 32), (16, 0), (1, 3)])
+def test_topk16_v4_forced_rescans_and_compactions(K, V4, stride, rank):
+    """rank 1 and stride 1 (rank 3): estimates far above the k-th score, so most queries
+    fail verification and their blocks rescan; rank 32 of a 1/32 sample: a low
+    threshold that overflows buffers (streamed compactions); rank 0: no sample,
+    a running threshold from -inf (compaction-driven). All bit-exact."""
+    V4(stride, rank)
+    rng = np.random.default_rng(stride * 100 + rank)
+    _check(K, _dyadic(rng, 520, 128), _dyadic(rng, 24000, 128), 100, torch.float16)
+
+
+def test_topk16_v4_massive_ties_and_exclusion(K, V4):
+    """Thousands of exact ties per score (compactions resolved into the ids,
+    strict thresholds) with an exclusion bitmap and an id offset."""
+    V4(8, 0)
+    rng = np.random.default_rng(5)
+    base = _dyadic(rng, 40, 128)
+    x = base[rng.integers(0, 40, size=20000)]
+    q = _dyadic(rng, 300, 128)
+    excl = [rng.choice(20000, int(rng.integers(0, 3000)), replace=False) for _ in range(300)]
+    _check(K, q, x, 100, torch.float16, exclude=excl, id_offset=7_000_000)
+    V4()
+    _check(K, q, x, 64, torch.bfloat16, exclude=excl)

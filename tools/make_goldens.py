@@ -352,6 +352,68 @@ def gen_reference_r2(ref: Path, out: Path):
           **{f"b1_{k}": v for k, v in batches[1].items()})
 
 
+def gen_reference_r3(ref: Path, out: Path):
+    """Round-3 fixture: the reference generate_recommendations on heavy users
+    (more train items than top_k leaves eligible), whose lists the reference
+    pads with its -inf train items (scripts/evaluate_model.py:224-232)."""
+    sys.path.insert(0, str(HERE / "loguru_stub"))
+    sys.path.insert(0, str(ref))
+    from src.training.utils import create_two_tower_model_for_training  # noqa: E402
+
+    import importlib.util
+
+    print("reference generate_recommendations on heavy users (padded lists)")
+    spec = importlib.util.spec_from_file_location("ref_evaluate_model", ref / "scripts" / "evaluate_model.py")
+    evm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(evm)
+    torch.manual_seed(41)
+    m = create_two_tower_model_for_training(3, 20, {"embedding_dim": 64, "hidden_layers": [128, 64],
+                                                    "dropout_rate": 0.2, "temperature": 0.05})
+    _randomize_bn(m, torch.Generator().manual_seed(42))
+    m.eval()
+    rng = np.random.default_rng(43)
+    n_items, n_users = 160, 120
+    uf = rng.standard_normal((n_users, 3)).astype(np.float32)
+    mf = (rng.random((n_items, 20)) < 0.15).astype(np.float32)
+    mf[:, 18:] = rng.random((n_items, 2)).astype(np.float32)
+    test_users = sorted(rng.choice(n_users, 60, replace=False).tolist())
+    # 0..150 train items: most users leave fewer than 100 eligible items
+    train_items = {u: sorted(rng.choice(n_items, int(rng.integers(0, 151)), replace=False).tolist())
+                   for u in test_users}
+    recs = evm.generate_recommendations(m, test_users, train_items, uf, mf, top_k=100, batch_size=256)
+    excl = np.full((len(test_users), 160), -1, np.int64)
+    for r, u in enumerate(test_users):
+        excl[r, :len(train_items[u])] = train_items[u]
+    _save(out, "eval_topk_heavy", **_state_arrays("user", m.user_tower), **_state_arrays("item", m.item_tower),
+          user_features=uf, movie_features=mf, test_users=np.array(test_users, np.int64), exclude=excl,
+          recs=np.array([recs[u] for u in test_users], np.int64))
+
+    print("reference Adam moments after the step that follows ckpt_ref_trainer.pth")
+    from src.training.trainers.two_tower import TwoTowerTrainer  # noqa: E402
+    ck = torch.load(out / "ckpt_ref_trainer.pth", map_location="cpu", weights_only=True)
+    with np.load(out / "ckpt_ref_expect.npz", allow_pickle=False) as z:
+        b1 = {k[3:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("b1_")}
+    model = create_two_tower_model_for_training(3, 20, {"embedding_dim": 64, "hidden_layers": [128, 64],
+                                                        "dropout_rate": 0.0, "temperature": 0.05})
+    model.user_tower.load_state_dict(ck["user_tower_state"])
+    model.item_tower.load_state_dict(ck["item_tower_state"])
+    with torch.no_grad():
+        model.user_bias.copy_(ck["user_bias"])
+        model.item_bias.copy_(ck["item_bias"])
+    with tempfile.TemporaryDirectory() as td:
+        trainer = TwoTowerTrainer(model, [b1], [b1], {"learning_rate": 1e-3, "weight_decay": 1e-5,
+                                                      "checkpoint_dir": td})
+        trainer.optimizer.load_state_dict(ck["optimizer_state"])
+        trainer.train_epoch(2)
+    st = trainer.optimizer.state_dict()["state"]
+    moments = {}
+    for i, v in st.items():
+        moments[f"exp_avg/{i}"] = v["exp_avg"].numpy()
+        moments[f"exp_avg_sq/{i}"] = v["exp_avg_sq"].numpy()
+        moments[f"step/{i}"] = np.float64(float(v["step"]))
+    _save(out, "ckpt_ref_moments", **moments)
+
+
 def _dyadic_unit(rng, n, d, nnz=16):
     """Unit-norm rows with `nnz` entries of ±1/4 (nnz=16): the renorm is exactly
     the identity and every inner product is an exact multiple of 1/16."""
@@ -418,7 +480,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--out", default=str(HERE.parent / "tests" / "golden"))
-    ap.add_argument("--only", choices=["reference", "dyadic", "r2"], default=None)
+    ap.add_argument("--only", choices=["reference", "dyadic", "r2", "r3"], default=None)
     a = ap.parse_args()
     out = Path(a.out)
     if a.only in (None, "dyadic"):
@@ -433,6 +495,10 @@ def main():
         ref = Path(a.ref)
         if (ref / "src" / "models" / "two_tower.py").exists():
             gen_reference_r2(ref, out)
+    if a.only in (None, "reference", "r3"):
+        ref = Path(a.ref)
+        if (ref / "src" / "models" / "two_tower.py").exists():
+            gen_reference_r3(ref, out)
 
 
 if __name__ == "__main__":
