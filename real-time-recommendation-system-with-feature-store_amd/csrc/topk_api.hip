@@ -226,6 +226,7 @@ inline Plan make_plan(int64_t nq, int64_t nx, int d, int dtype, int k, const Sha
     p.items_per_split = tiles_per * sh.nt;
     p.splits = static_cast<int>(nx > 0 ? (nx + p.items_per_split - 1) / p.items_per_split : 1);
     p.cap = sh.cap;
+    p.kth_bytes = (sh.kind == 0 && p.splits > 1) ? static_cast<size_t>(p.chunk) * sizeof(uint32_t) : 0;
     p.cand_bytes = static_cast<size_t>(p.splits) * p.q_tiles * sh.qt * p.cap * sizeof(Cand);
     p.part_bytes = p.splits > 1 ? static_cast<size_t>(p.splits) * p.chunk * k * (sizeof(float) + sizeof(int64_t)) : 0;
     return p;
@@ -242,7 +243,8 @@ extern "C" size_t rt_flatip_topk_workspace_bytes(int64_t nq, int64_t nx, int d, 
     if (nq <= 0 || k <= 0 || k > topk::kMaxK || d <= 0) return 256;
     if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return 256;
     const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
-    return topk::align256(p.cand_bytes) + p.part_bytes + topk::align256(p.meta_bytes) + 256;
+    return topk::align256(p.cand_bytes) + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes) +
+           256;
 }
 
 extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
@@ -260,10 +262,13 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     if (exclude_bits && exclude_words < (nx + 31) / 32) return RT_ERR_INVALID;
     const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
     const size_t cand_al = topk::align256(p.cand_bytes);
-    if (!workspace || workspace_bytes < cand_al + p.part_bytes + topk::align256(p.meta_bytes)) return RT_ERR_WORKSPACE;
+    if (!workspace ||
+        workspace_bytes < cand_al + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes))
+        return RT_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
     char* part = reinterpret_cast<char*>(workspace) + cand_al;
     int* meta = reinterpret_cast<int*>(part + p.part_bytes);
+    uint32_t* kth = reinterpret_cast<uint32_t*>(part + p.part_bytes + topk::align256(p.meta_bytes));
     const size_t esz = dtype == RT_F32 ? 4 : 2;
     for (int64_t q0 = 0; q0 < nq; q0 += p.chunk) {
         const int64_t nc = (nq - q0) < p.chunk ? (nq - q0) : p.chunk;
@@ -287,6 +292,14 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
         a.cand = reinterpret_cast<Cand*>(workspace);
         a.id_offset = id_offset;
         a.meta = meta;
+        if (p.kth_bytes) {
+            a.kth_shared = kth;
+            const hipError_t e = hipMemsetAsync(kth, 0, static_cast<size_t>(nc) * sizeof(uint32_t), st);
+            if (e != hipSuccess) {
+                set_last_error("hipMemsetAsync(topk kth)", e);
+                return RT_ERR_HIP;
+            }
+        }
         if (p.splits > 1 && !p.v4) {  // per-split lists [split][nc][k], merged below
             a.out_s = reinterpret_cast<float*>(part);
             a.out_i = reinterpret_cast<int64_t*>(part + static_cast<size_t>(p.splits) * p.chunk * k * sizeof(float));

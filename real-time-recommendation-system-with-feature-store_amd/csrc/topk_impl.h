@@ -101,6 +101,7 @@ struct Plan {
     int v4;              // 1: the sampled-threshold scan + finish pair (topk_v4.h)
     int stride, rank;    // v4 sample: every stride-th stage; threshold = rank-th group maximum
     size_t meta_bytes;   // v4 per-(split, query, half) entry counts
+    size_t kth_bytes;    // register-list kernel over > 1 split: the shared per-query k-th keys
 };
 
 struct Args {
@@ -108,7 +109,17 @@ struct Args {
     const uint32_t* excl; int64_t excl_words;
     Cand* cand; float* out_s; int64_t* out_i; int64_t id_offset;
     int* meta;
+    uint32_t* kth_shared;  // register-list kernel, split corpora: per query, the best split k-th score (okey)
 };
+
+// order-preserving key of a score (-0 folded onto +0); 0 sorts below every score
+__device__ __forceinline__ uint32_t score_key(float s) {
+    const uint32_t u = __float_as_uint(s + 0.0f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float score_of_key(uint32_t k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
 
 __device__ __forceinline__ int tile_row(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
@@ -211,6 +222,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     };
     fetch(i_begin);
 
+    // k-th of a lane's sorted list (k <= K, runtime): a select chain
+    auto kth_of = [&](const float (&l)[K]) {
+        float v = l[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i) v = (i == k - 1) ? l[i] : v;
+        return v;
+    };
+    // cross-split k-th: the value the previous tile's atomic max returned
+    // (half-0 lanes; consumed one tile later, so the atomic's latency hides
+    // behind a tile of MFMAs)
+    uint32_t ret_key[QS];
+#pragma unroll
+    for (int j = 0; j < QS; ++j) ret_key[j] = 0u;
     for (int64_t t0 = i_begin; t0 < i_end; t0 += NT) {
         __syncthreads();  // previous tile consumed
 #pragma unroll
@@ -223,6 +247,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             }
         }
         __syncthreads();
+        if (t0 != i_begin) {
+            // Tighten each query's filter (any value <= the final k-th of this
+            // split's lists is valid; inserts stay strict >). Own list: its k-th,
+            // not its K-th. The partner half (lane ^ 32): its k-th too — its
+            // items precede every later item of mine, so an equal later score
+            // loses by id. Other splits: their k-th is <= the global k-th, but
+            // their ids may be larger than mine, so ties must still enter — one
+            // float step below it.
+#pragma unroll
+            for (int j = 0; j < QS; ++j) {
+                float t = kth_of(ls[j]);
+                t = fmaxf(t, __shfl_xor(t, 32, 64));
+                if (a.kth_shared) {
+                    const uint32_t prev = static_cast<uint32_t>(__shfl(static_cast<int>(ret_key[j]), col, 64));
+                    const float mine = t;
+                    if (prev) t = fmaxf(t, nextafterf(score_of_key(prev), -INFINITY));
+                    const int64_t q = qb + j * 32 + col;
+                    if (half == 0 && qok[j] && mine > -INFINITY)
+                        ret_key[j] = atomicMax(a.kth_shared + q, score_key(mine));
+                }
+                if (qok[j] && t > th[j]) th[j] = t;
+            }
+        }
         if (t0 + NT < i_end) fetch(t0 + NT);  // overlaps the MFMA work below
 #pragma unroll 1
         for (int rt = 0; rt < NT / 32; ++rt) {

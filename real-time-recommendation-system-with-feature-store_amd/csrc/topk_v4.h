@@ -33,9 +33,10 @@
 //    Each (split, query, half) writes its entry count to `meta`.
 // 2. flatip_topk_v4_finish: one wave per query over the union of its split
 //    buffers: a radix select on the composite key (order-preserving score
-//    key << 32 | ~id, larger = better: score desc, id asc) down to <= 1024
-//    survivors (usually k plus a few after 16 bits), one register bitonic
-//    sort, the k best written in Faiss order with (-FLT_MAX, -1) padding.
+//    key << 32 | ~id, larger = better: score desc, id asc) down to <= 128
+//    survivors (usually k plus a few after 16 bits), one 128-entry register
+//    bitonic sort, the k best written in Faiss order with (-FLT_MAX, -1)
+//    padding.
 //    The split merge is part of this pass (no topk_merge launch).
 #pragma once
 
@@ -49,7 +50,7 @@ constexpr int kHalf = kCap / 2;        // per owning lane half
 constexpr int kMaxK = 128;
 constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
 constexpr int kMaxSplits = 8;
-constexpr int kFinishCap = 1024;       // survivors a finish wave sorts at once
+constexpr int kFinishCap = 128;        // survivors a finish wave sorts at once (2 per lane)
 
 template <int QS>
 struct Geo {
@@ -69,9 +70,8 @@ struct Cfg4 {
     static constexpr int MAXP = (PIECES + kWavesB - 1) / kWavesB;
     static constexpr int TILE_BYTES = SLOTS * 16;
     static constexpr int RING = 3;
-    static constexpr int SCR_BYTES = kWavesB * 64 * 80;   // per-lane score rows (80 B: conflict-free b128)
     static constexpr int HIST_BYTES = kWavesB * 1024;
-    static constexpr int LDS_BYTES = RING * TILE_BYTES + SCR_BYTES + HIST_BYTES + 16;
+    static constexpr int LDS_BYTES = RING * TILE_BYTES + HIST_BYTES + 16;
     static_assert(PIECES * 64 == SLOTS, "whole DMA pieces");
     static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
@@ -243,8 +243,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     constexpr int QT = Geo<QS>::QT;
     __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
     char* const ring = lds;
-    float* const scr = reinterpret_cast<float*>(lds + C::RING * C::TILE_BYTES);
-    uint32_t* const hist_all = reinterpret_cast<uint32_t*>(lds + C::RING * C::TILE_BYTES + C::SCR_BYTES);
+    uint32_t* const hist_all = reinterpret_cast<uint32_t*>(lds + C::RING * C::TILE_BYTES);
     uint32_t* const flag = hist_all + kWavesB * 256;
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
@@ -261,7 +260,6 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     const int64_t q_pad = static_cast<int64_t>(gridDim.x / splits) * QT;
     Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32·QS buffers
     uint32_t* const whist = hist_all + wave * 256;
-    float* const wscr = scr + (wave * 64 + lane) * 20;
     const int nst = i_end > i_begin ? static_cast<int>((i_end - i_begin + C::NT - 1) / C::NT) : 0;
     const int nsa = (rank > 0 && stride > 0) ? (nst + stride - 1) / stride : 0;  // sample stages
     if (tid == 0) *flag = 0u;
@@ -359,46 +357,36 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         for (int r = 3; r < 15; r += 2) m = fmaxf(fmaxf(m, acc[r]), acc[r + 1]);
         return fmaxf(m, acc[15]);
     };
-    auto appends = [&](int j, const f32x16& acc, int64_t sub0, float m) {
-        if (__ballot(m >= thr[j]) == 0) return;
-        uint32_t bits = 0u;  // bit 15-r <=> acc[r] passes
+    // Appends of one sub-tile for query set j: row by row, the wave mask of
+    // the lanes whose score passes (one v_cmp into SGPRs); a row no lane
+    // passes is skipped by a scalar branch, otherwise its passing lanes store
+    // (score, id) at their cursors (two SADDR dword stores). With 64
+    // independent queries per wave almost every sub-tile has SOME passing
+    // lane, so this path is the common one: ~16 compares and a few store
+    // blocks, no per-lane loop, no LDS round trip.
+    auto appends = [&](int j, const f32x16& acc, int64_t sub0) {
         const float t = thr[j];
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-            asm("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
-                : "+v"(bits)
-                : "v"(acc[r]), "v"(t)
-                : "vcc");
-        if constexpr (EXCL) {
-            if (excl[j]) {
-                const uint32_t xw = excl[j][sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if ((xw >> tile_row(r, half)) & 1u) bits &= ~(1u << (15 - r));
-            }
-        }
-        if (bits) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                *reinterpret_cast<float4*>(wscr + 4 * i) =
-                    make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
-        }
         const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
+        uint32_t xw = 0u;
+        if constexpr (EXCL) {
+            if (excl[j]) xw = excl[j][sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
+        }
         uint32_t wo = woff[j];
-        while (__ballot(bits != 0u)) {
-            issued += 2;  // exactly two store instructions for the wave
-            if (bits) {
-                const int b = 31 - __builtin_clz(bits);  // highest set bit = lowest r
-                bits &= ~(1u << b);
-                const int r = 15 - b;
-                const float v = wscr[r];  // same-wave LDS write → read: in order
-                const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
-                asm volatile(
-                    "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
-                    "v_add_u32 %0, 8, %0"
-                    : "+v"(wo)
-                    : "v"(v), "s"(wbase), "v"(id)
-                    : "memory");
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            bool pass = acc[r] >= t;
+            if constexpr (EXCL) pass = pass && !((xw >> tile_row(r, half)) & 1u);
+            if (__ballot(pass)) {
+                issued += 2;  // exactly two store instructions for the wave
+                if (pass) {
+                    const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
+                    asm volatile(
+                        "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
+                        "v_add_u32 %0, 8, %0"
+                        : "+v"(wo)
+                        : "v"(acc[r]), "s"(wbase), "v"(id)
+                        : "memory");
+                }
             }
         }
         woff[j] = wo;
@@ -478,6 +466,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         raw_barrier();
     };
 
+    RT_PT(uint64_t pc_wait = 0, pc_bar = 0, pc_main = 0, pc_samp = 0, pc_cmp = 0; const uint64_t pc_start = clock64();)
     if (nsa > 0) {
         prologue(nsa, true);
         int cur = 0;
@@ -515,6 +504,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             for (int i = 0; i + 1 < C::RING - 1; ++i) mk[i] = mk[i + 1];
             cur = cur == C::RING - 1 ? 0 : cur + 1;
         }
+        RT_PT(pc_samp = clock64() - pc_start;)
 #pragma unroll
         for (int j = 0; j < QS; ++j) {
             const float e = union_rank(L[j], rank);
@@ -541,82 +531,68 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             if (v + C::RING - 1 < nst) fetch(stage_t0(v + C::RING - 1, false), cur == 0 ? C::RING - 1 : cur - 1);
             mk[C::RING - 2] = issued;
             const char* stage = ring + cur * C::TILE_BYTES + a_lane;
+            RT_PT(const uint64_t c0 = clock64();)
 #pragma unroll
             for (int rt = 0; rt < C::NSUB; ++rt) {
                 if (rt * 32 < rem) {
                     const int64_t sub0 = t0 + rt * 32;
-                    const bool next_here = rt + 1 < C::NSUB && (rt + 1) * 32 < rem;
-                    // set 0: MFMAs, with the previous sub-tile's last set reduced in the gaps
-                    float mp = 0.f;
+                    // set 0: MFMAs; the previous sub-tile's last set is filtered behind them
                     acc[0] = f32x16{};
 #pragma unroll
-                    for (int s = 0; s < S; ++s) {
-                        acc[0] = M::run(af[s], qf[0][s], acc[0]);
-                        if constexpr (QS > 1) {
-                            const f32x16& p = acc[QS - 1];
-                            if (s == 0) mp = fmaxf(fmaxf(p[0], p[1]), p[2]);
-                            if (s == 1) mp = fmaxf(fmaxf(mp, p[3]), p[4]);
-                            if (s == 2) mp = fmaxf(fmaxf(mp, p[5]), p[6]);
-                            if (s == 3) mp = fmaxf(fmaxf(mp, p[7]), p[8]);
-                            if (s == 4 || (S < 8 && s == S - 1)) {
-                                mp = fmaxf(fmaxf(mp, p[9]), p[10]);
-                                mp = fmaxf(fmaxf(mp, p[11]), p[12]);
-                                mp = fmaxf(fmaxf(mp, p[13]), p[14]);
-                                mp = fmaxf(mp, p[15]);
-                            }
-                        }
-                    }
-                    if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev, mp);
+                    for (int s = 0; s < S; ++s) acc[0] = M::run(af[s], qf[0][s], acc[0]);
+                    if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev);
                     if (rem < (rt + 1) * 32) mask_tail(acc[0], sub0);
                     if constexpr (QS == 1) {
-                        if (next_here) lds_a(af, stage, rt + 1);
+                        if (rt + 1 < C::NSUB) lds_a(af, stage, rt + 1);
                     }
 #pragma unroll
                     for (int j = 1; j < QS; ++j) {
-                        float m0 = 0.f;
                         acc[j] = f32x16{};
 #pragma unroll
                         for (int s = 0; s < S; ++s) {
                             acc[j] = M::run(af[s], qf[j][s], acc[j]);
-                            if (j == QS - 1 && next_here)  // fragment s is free once its last MFMA issued
+                            // fragment s is free once its last MFMA issued; rows past a
+                            // partial stage's end are stale but finite and never filtered in
+                            if (j == QS - 1 && rt + 1 < C::NSUB)
                                 af[s] = __builtin_bit_cast(
                                     frag, *reinterpret_cast<const uint4*>(stage + (rt + 1) * 32 * C::RS + s * 32));
-                            const f32x16& p = acc[j - 1];
-                            if (s == 0) m0 = fmaxf(fmaxf(p[0], p[1]), p[2]);
-                            if (s == 1) m0 = fmaxf(fmaxf(m0, p[3]), p[4]);
-                            if (s == 2) m0 = fmaxf(fmaxf(m0, p[5]), p[6]);
-                            if (s == 3) m0 = fmaxf(fmaxf(m0, p[7]), p[8]);
-                            if (s == 4 || (S < 8 && s == S - 1)) {
-                                m0 = fmaxf(fmaxf(m0, p[9]), p[10]);
-                                m0 = fmaxf(fmaxf(m0, p[11]), p[12]);
-                                m0 = fmaxf(fmaxf(m0, p[13]), p[14]);
-                                m0 = fmaxf(m0, p[15]);
-                            }
                         }
-                        appends(j - 1, acc[j - 1], sub0, m0);
+                        appends(j - 1, acc[j - 1], sub0);
                         if (rem < (rt + 1) * 32) mask_tail(acc[j], sub0);
                     }
-                    if constexpr (QS == 1) appends(0, acc[0], sub0, max16(acc[0]));
+                    if constexpr (QS == 1) appends(0, acc[0], sub0);
                     sub_prev = sub0;
                 }
             }
+            RT_PT(const uint64_t c1 = clock64(); pc_main += c1 - c0;)
             if (more) wait_vm_le(issued - mk[0]);
+            RT_PT(const uint64_t c2 = clock64(); pc_wait += c2 - c1;)
             raw_barrier();
+            RT_PT(const uint64_t c3 = clock64(); pc_bar += c3 - c2;)
 #pragma unroll
             for (int i = 0; i + 1 < C::RING - 1; ++i) mk[i] = mk[i + 1];
             cur = cur == C::RING - 1 ? 0 : cur + 1;
             if (more) {
                 maybe_compact();  // the only check in the loop: between stages, before any fragment is live
+                RT_PT(pc_cmp += clock64() - c3;)
                 lds_a(af, ring + cur * C::TILE_BYTES + a_lane, 0);
             }
         }
-        if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev, max16(acc[QS - 1]));
+        if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev);
         maybe_compact();
     };
+#ifdef RT_TOPK_PROBE_NOSEL
+#pragma unroll
+    for (int j = 0; j < QS; ++j) thr[j] = INFINITY;  // probe builds only: the scan without appends
+#endif
     main_pass();
 
     // ---- verification: a sampled threshold that left < k entries rescans ----
+#ifdef RT_TOPK_PROBE_NOSEL
+    if (false) {
+#else
     if (nsa > 0) {
+#endif
         bool any = false;
 #pragma unroll
         for (int j = 0; j < QS; ++j) {
@@ -642,6 +618,15 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
         meta[((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * 2 + half] = cnt;
     }
+#ifdef RT_TOPK_PROBE_TIMING
+    {  // [total, DMA wait, barrier, main sub-tiles, sample pass, compaction checks]
+        const int64_t gw = static_cast<int64_t>(blockIdx.x) * kWavesB + wave;
+        if (lane == 0 && gw < 65536) {
+            uint64_t* o = v3::probe_cycles + gw * 6;
+            o[0] = clock64() - pc_start; o[1] = pc_wait; o[2] = pc_bar; o[3] = pc_main; o[4] = pc_samp; o[5] = pc_cmp;
+        }
+    }
+#endif
 }
 
 // ---- finish: radix select over the union of a query's split buffers ----
@@ -739,10 +724,7 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
     }
     if (m > kFinishCap) m = kFinishCap;  // cannot happen: the prefix bounds it
     wave_lds_sync();
-    if (m <= 128) finish_sort<2>(keep, m, k, os, oi, id_offset);
-    else if (m <= 256) finish_sort<4>(keep, m, k, os, oi, id_offset);
-    else if (m <= 512) finish_sort<8>(keep, m, k, os, oi, id_offset);
-    else finish_sort<16>(keep, m, k, os, oi, id_offset);
+    finish_sort<2>(keep, m, k, os, oi, id_offset);
 }
 
 template <typename T, int S, int QS>

@@ -12,13 +12,14 @@
   the whole corpus.
 * Table-sharded row gather (config C5): the owner of row ``id`` is the rank
   whose contiguous range holds it; the batch ids are all-gathered, every rank
-  gathers the rows it owns (in batch order) into one segment, the segments are
-  all-gathered and a permutation gather puts every row in batch order on every
-  rank (copies only).
+  gathers the whole batch against its own window (zero rows elsewhere) and one
+  byte-wise MAX all-reduce leaves every owner's rows everywhere (copies only,
+  no host synchronisation, graph-capturable).
 * Data-parallel in-batch step of config C5 (:func:`sharded_inbatch_step`):
   each rank scores its own users against the whole gathered batch of items;
-  for a trainable table the item-row gradients go back to their owners with
-  one reduce-scatter (:func:`sharded_scatter_add_rows`).
+  the table is frozen as in the reference (no item-gradient exchange), or, for
+  a trainable table, the item-row gradients are summed and added by their
+  owners (:func:`sharded_scatter_add_rows`).
 * Data-parallel training: the flat fp32 grad slab is averaged with one
   all-reduce (see training/fused_step.py).
 
@@ -123,58 +124,84 @@ def sharded_topk_owner(queries: torch.Tensor, k: int, local_topk: TopkFn, merge:
     return merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
 
 
+def _exchange_rows(local: torch.Tensor, group) -> torch.Tensor:
+    """Every rank holds [P, D] rows that are zero except at the positions it owns
+    (exactly one owner per valid position): the max over ranks of the raw BYTES
+    (non-owners contribute 0x00) is the owner's row bit for bit — including
+    -0.0 and NaN payloads, which a float sum would not preserve. One all-reduce
+    (uint8 MAX; RCCL ncclUint8), no host synchronisation."""
+    flat = local.contiguous().view(torch.uint8)
+    dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=group)
+    return local
+
+
 def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Tensor, group=None,
-                        gather: Optional[Callable] = None) -> torch.Tensor:
+                        gather: Optional[Callable] = None, counts: Optional[Sequence[int]] = None,
+                        status: Optional[torch.Tensor] = None, check: bool = False,
+                        return_ids: bool = False):
     """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL
     batch (all ranks' ``ids`` concatenated in rank order) on every rank.
 
-    Owner-segment exchange: one all-gather of (count, window) metadata and one
-    of the batch ids; every rank gathers the rows IT owns, in batch order, into
-    a segment padded to the largest owner's count; one all-gather of those
-    segments and a permutation gather (segment of owner o, slot = rank of the
-    position among o's positions) put the rows in batch order. Every row moves
-    once per receiving rank and is copied, never summed, so the result is
-    bit-identical to a single-table gather. ``gather(table, ids, row_begin)``
-    returns [len(ids), dim] (``rt_gather_rows`` semantics, the default)."""
-    gather = gather or (lambda t, i, b: kernels.gather_rows(t, i, row_begin=b))
+    Sync-free, graph-capturable exchange (no device→host read anywhere):
+    one all-gather of the batch ids (each rank's ids padded to the batch width
+    with -1); every rank gathers the WHOLE global batch against its own row
+    window (``rt_gather_rows`` with ``row_begin``: ids outside the window, and
+    the -1 padding, give zero rows and are counted as out-of-window); one
+    all-reduce of the rows' bytes (:func:`_exchange_rows`) leaves every
+    position holding its owner's row. Rows are copied, never summed, so the
+    result is bit-identical to a single-table gather.
+
+    ``counts``: per-rank batch sizes when they differ (host data, e.g. the last
+    ragged batch); by default every rank's batch has this rank's size (the C5
+    step). ``status`` (int64 [2], device, optional): accumulates (positions,
+    positions owned by some rank); they differ iff some id lies outside every
+    window — the id-range check without a sync. ``check=True`` reads it and
+    raises IndexError (one sync). ``gather(table, ids, row_begin)`` returns
+    [len(ids), dim] with zero rows outside the window, as ``rt_gather_rows``
+    does (the default). ``return_ids``: also return the global ids (-1 padding
+    removed)."""
+    gather_fn = gather
+    oob = None
+    if gather_fn is None:
+        oob = torch.zeros(1, dtype=torch.int32, device=ids.device)
+        gather_fn = lambda t, i, b: kernels.gather_rows(t, i, row_begin=b, oob=oob)  # noqa: E731
     world, rank = _world(group)
-    if world == 1:
-        return gather(table_shard, ids, row_begin)
-    dev = ids.device
-    meta = torch.tensor([ids.numel(), int(row_begin), int(row_begin) + table_shard.shape[0]], dtype=torch.int64,
-                        device=dev)
-    all_meta = torch.empty(world * 3, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(all_meta, meta, group=group)
-    all_meta = all_meta.view(world, 3)
-    counts = [int(c) for c in all_meta[:, 0].tolist()]
-    width = max(counts)
-    if width == 0:
-        return torch.empty((0, table_shard.shape[1]), dtype=table_shard.dtype, device=table_shard.device)
-    padded = torch.full((width,), -1, dtype=torch.int64, device=dev)
-    padded[: ids.numel()] = ids.to(torch.int64)
-    all_ids = torch.empty((world * width,), dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(all_ids, padded, group=group)
-    keep = torch.cat([torch.arange(r * width, r * width + c, device=dev) for r, c in enumerate(counts)])
-    global_ids = all_ids[keep]
-    # owner of each position: the rank whose [begin, end) window holds the id
-    begins = all_meta[:, 1].contiguous()
-    owner = torch.searchsorted(begins, global_ids, right=True) - 1
-    bad = (owner < 0) | (global_ids >= all_meta[owner.clamp(min=0), 2])
-    if bool(bad.any()):
-        raise IndexError("batch id outside every rank's table window")
-    per_owner = torch.bincount(owner, minlength=world)
-    seg = int(per_owner.max())
-    send = torch.zeros((seg, table_shard.shape[1]), dtype=table_shard.dtype, device=table_shard.device)
-    mine = torch.nonzero(owner == rank).flatten()
-    if mine.numel():
-        send[: mine.numel()] = gather(table_shard, global_ids[mine], row_begin)
-    segs = torch.empty((world * seg, table_shard.shape[1]), dtype=table_shard.dtype, device=table_shard.device)
-    dist.all_gather_into_tensor(segs, send, group=group)
-    order = torch.argsort(owner, stable=True)
-    starts = torch.cumsum(per_owner, 0) - per_owner
-    slot = torch.empty_like(owner)
-    slot[order] = torch.arange(owner.numel(), device=dev) - starts[owner[order]]
-    return gather(segs, owner * seg + slot, 0)
+    ids = ids.to(torch.int64)
+    width = max(counts) if counts is not None else ids.numel()
+    if counts is not None and ids.numel() != counts[rank]:
+        raise ValueError(f"rank {rank} holds {ids.numel()} ids, counts say {counts[rank]}")
+    if world > 1:
+        padded = ids
+        if ids.numel() != width:
+            padded = torch.full((width,), -1, dtype=torch.int64, device=ids.device)
+            padded[: ids.numel()] = ids
+        all_ids = torch.empty((world * width,), dtype=torch.int64, device=ids.device)
+        dist.all_gather_into_tensor(all_ids, padded.contiguous(), group=group)
+    else:
+        all_ids = ids
+    rows = gather_fn(table_shard, all_ids, row_begin)
+    n_valid = sum(counts) if counts is not None else world * width
+    if status is not None or check:
+        if oob is not None:
+            owned = all_ids.numel() - oob.to(torch.int64)
+        else:
+            loc = all_ids - int(row_begin)
+            owned = ((loc >= 0) & (loc < table_shard.shape[0])).sum().reshape(1)
+        if world > 1:
+            dist.all_reduce(owned, op=dist.ReduceOp.SUM, group=group)
+        # (no host→device copy: capturable) positions, positions owned by some rank
+        st = torch.cat([torch.full((1,), n_valid, dtype=torch.int64, device=ids.device), owned])
+        if status is not None:
+            status += st
+        if check and int(st[0]) != int(st[1]):
+            raise IndexError("batch id outside every rank's table window")
+    if world > 1:
+        rows = _exchange_rows(rows, group)
+    if counts is not None and any(c != width for c in counts):  # drop the padding (host-known positions)
+        keep = torch.cat([torch.arange(r * width, r * width + c, device=ids.device) for r, c in enumerate(counts)])
+        rows = rows.index_select(0, keep)
+        all_ids = all_ids.index_select(0, keep)
+    return (rows, all_ids) if return_ids else rows
 
 
 def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_ids: torch.Tensor,
@@ -182,74 +209,56 @@ def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_id
                              scatter_add: Optional[Callable] = None) -> torch.Tensor:
     """Backward of :func:`sharded_gather_rows` for a TRAINABLE row-sharded table
     (the nn.Embedding path a2 under C5 sharding, SURVEY §8(e) "next"): every rank
-    holds its d loss / d rows for the whole global batch (``grad_rows`` [B_total,
-    D], rows in the order of ``global_ids``); the owner of each row receives the
-    sum over ranks and adds it into its shard's gradient (``grad_shard`` [rows,
-    D], shard rows start at global ``row_begin``).
+    holds its own contribution to d loss / d rows for the whole global batch
+    (``grad_rows`` [B_total, D], rows in the order of ``global_ids``); the owner
+    of each row adds the sum over ranks into its shard's gradient
+    (``grad_shard`` [rows, D], shard rows start at global ``row_begin``).
 
-    One reduce-scatter moves each row's gradient once per rank: positions are
-    ordered by owner (stable), each owner's segment padded to the largest
-    segment, summed over ranks by ``reduce_scatter_tensor`` (an all-reduce of the
-    same buffer on gloo, which has no reduce-scatter), and the owner's segment is
-    scatter-added (``rt_scatter_add_rows_f32``; repeated ids accumulate)."""
+    Sync-free: one all-reduce (sum) of the row gradients, then every rank
+    scatter-adds the rows of its own window (``rt_scatter_add_rows_f32`` skips
+    ids outside [0, rows); repeated ids accumulate)."""
     scatter_add = scatter_add or (lambda t, ids, g: kernels.scatter_add_rows(t, ids, g))
-    world, rank = _world(group)
-    ids = global_ids.to(torch.int64)
-    if world == 1:
-        return scatter_add(grad_shard, ids - row_begin, grad_rows)
-    dev = ids.device
-    win = torch.tensor([int(row_begin), int(row_begin) + grad_shard.shape[0]], dtype=torch.int64, device=dev)
-    all_win = torch.empty(world * 2, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(all_win, win, group=group)
-    all_win = all_win.view(world, 2)
-    owner = torch.searchsorted(all_win[:, 0].contiguous(), ids, right=True) - 1
-    if bool(((owner < 0) | (ids >= all_win[owner.clamp(min=0), 1])).any()):
-        raise IndexError("batch id outside every rank's table window")
-    per_owner = torch.bincount(owner, minlength=world)
-    seg = int(per_owner.max())
-    if seg == 0:
-        return grad_shard
-    order = torch.argsort(owner, stable=True)
-    starts = torch.cumsum(per_owner, 0) - per_owner
-    slot = torch.arange(ids.numel(), device=dev) - starts[owner[order]]
-    d = grad_rows.shape[1]
-    send = torch.zeros((world * seg, d), dtype=grad_rows.dtype, device=grad_rows.device)
-    send[owner[order] * seg + slot] = grad_rows[order]
-    recv = torch.empty((seg, d), dtype=grad_rows.dtype, device=grad_rows.device)
-    if dist.get_backend(group) == "gloo":
-        dist.all_reduce(send, op=dist.ReduceOp.SUM, group=group)
-        recv.copy_(send[rank * seg:(rank + 1) * seg])
-    else:
-        dist.reduce_scatter_tensor(recv, send, op=dist.ReduceOp.SUM, group=group)
-    n_mine = int(per_owner[rank])
-    if n_mine:
-        mine_ids = ids[order[starts[rank]:starts[rank] + n_mine]]
-        scatter_add(grad_shard, mine_ids - row_begin, recv[:n_mine])
-    return grad_shard
+    world, _ = _world(group)
+    g = grad_rows
+    if world > 1:
+        g = grad_rows.contiguous().clone()
+        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+    return scatter_add(grad_shard, global_ids.to(torch.int64) - int(row_begin), g)
 
 
 def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: torch.Tensor,
                          item_ids: torch.Tensor, temperature: float, group=None,
-                         gather: Optional[Callable] = None, loss_fn: Optional[Callable] = None):
+                         gather: Optional[Callable] = None, loss_fn: Optional[Callable] = None,
+                         grad_shard: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None,
+                         scatter_add: Optional[Callable] = None):
     """Config C5 data-parallel in-batch step (SURVEY §8(e) training): the item
     table is row-sharded, every rank holds ``user_emb`` [b, D] for its own b
-    users and ``item_ids`` [b] of their positives. The global batch's item rows
-    are fetched with :func:`sharded_gather_rows` (one id all-gather + one
-    all-reduce), each rank scores its users against ALL gathered items (label of
-    local user i = global item rank·b + i) with ``rt_inbatch_loss_fwd_bwd``, and
-    the loss is averaged over ranks. Returns (global mean loss, d loss/d user_emb
-    for the local users, d loss/d item rows summed over ranks [B_total, D]) —
-    the latter is what the owners would scatter-add if the table were trainable
-    (in the reference it is a precomputed feature table, so it is not)."""
+    users and ``item_ids`` [b] of their positives (b equal on every rank). The
+    global batch's item rows come from :func:`sharded_gather_rows` (sync-free);
+    each rank scores its users against ALL gathered items (label of local user
+    i = global item rank·b + i) with ``rt_inbatch_loss_fwd_bwd``; the loss is
+    averaged over ranks (one 8-byte all-reduce).
+
+    The item table is a frozen feature table in the reference
+    (src/training/datasets/movielens.py:61-63,116), so by default the item-row
+    gradients are NOT exchanged: the third result is this rank's own
+    contribution [B_total, D]. With ``grad_shard`` (a trainable table) they are
+    summed and added into the owners' shards (:func:`sharded_scatter_add_rows`).
+    No host synchronisation at any world size, N = 1 included (the same code
+    runs; its collectives are skipped), so the whole step can be captured in a
+    hipGraph. Returns (global mean loss [1], d loss/d user_emb, d loss/d rows
+    (this rank's part))."""
     world, rank = _world(group)
     b = user_emb.shape[0]
-    rows = sharded_gather_rows(table_shard, row_begin, item_ids, group, gather)
+    rows, gids = sharded_gather_rows(table_shard, row_begin, item_ids, group, gather, status=status,
+                                     return_ids=True)
     loss_fn = loss_fn or (lambda u, p, off: kernels.inbatch_loss(u, p, temperature, label_offset=off))
     loss, du, dp = loss_fn(user_emb, rows, rank * b)
     lv = loss[0:1].clone()
     if world > 1:
         dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
-        dist.all_reduce(dp, op=dist.ReduceOp.SUM, group=group)
+    if grad_shard is not None:
+        sharded_scatter_add_rows(grad_shard, row_begin, gids, dp.float() / world, group, scatter_add)
     # each rank's loss is a mean over its own b users; the global mean averages them
     return lv / world, du / world, dp / world
 

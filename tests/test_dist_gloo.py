@@ -144,17 +144,39 @@ def _gather_worker(rank, world, n, d, seed, counts, skew):
         out[ok] = t[loc[ok]]
         return out
 
-    rows = sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=window_gather)
+    status = torch.zeros(2, dtype=torch.int64)
+    rows = sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=window_gather,
+                               counts=counts if len(set(counts)) > 1 else None, status=status)
     ref = table[np.concatenate(all_ids)]
     np.testing.assert_array_equal(rows.numpy(), ref)
+    assert status[0] == status[1] == sum(counts)  # every id owned by exactly one rank
+    # bit-exact through the byte-wise exchange: -0.0 and NaN payloads survive
+    special = table.copy()
+    special[::7, 0] = -0.0
+    special[1::7, 1] = np.float32("nan")
+    shard2 = torch.from_numpy(special[b:b + c])
+    rows2 = sharded_gather_rows(shard2, b, torch.from_numpy(all_ids[rank]), gather=window_gather,
+                                counts=counts if len(set(counts)) > 1 else None)
+    assert rows2.numpy().tobytes() == special[np.concatenate(all_ids)].tobytes()
+    # an id outside every window: counted (no sync) or raised with check=True
+    bad = torch.from_numpy(all_ids[rank]).clone()
+    if bad.numel():
+        bad[0] = n + 5
+    st = torch.zeros(2, dtype=torch.int64)
+    sharded_gather_rows(shard, b, bad, gather=window_gather, counts=counts if len(set(counts)) > 1 else None,
+                        status=st)
+    assert int(st[1]) == sum(counts) - sum(1 for cc in counts if cc)
+    with pytest.raises(IndexError):  # every rank with ids planted one bad id
+        sharded_gather_rows(shard, b, bad, gather=window_gather, counts=counts if len(set(counts)) > 1 else None,
+                            check=True)
 
 
 @pytest.mark.parametrize("world,counts,skew", [(2, [13, 29], False), (4, [7, 0, 31, 16], False),
                                                (2, [40, 9], True), (3, [5, 5, 5], True)])
 def test_sharded_gather_rows_gloo(world, counts, skew):
-    """C5 owner-segment exchange: ragged per-rank batches (one empty), ids
-    skewed onto one owner (empty segments elsewhere): rows in batch order,
-    bit-exact."""
+    """C5 sync-free exchange: ragged per-rank batches (one empty), ids skewed
+    onto one owner (the other windows own nothing): rows in batch order,
+    bit-exact (-0.0 and NaN payloads included); out-of-window ids counted."""
     _run(world, _gather_worker, 997, 16, 3, counts, skew)
 
 
@@ -169,8 +191,9 @@ def _scatter_worker(rank, world, n, d, b, seed):
     rb, rc = shard_range(n, world, rank)
     shard_grad = torch.zeros((rc, d))
 
-    def scatter_add(t, loc, g):  # rt_scatter_add_rows_f32 semantics on CPU
-        t.index_add_(0, loc, g)
+    def scatter_add(t, loc, g):  # rt_scatter_add_rows_f32 semantics on CPU: ids outside [0, rows) skipped
+        ok = (loc >= 0) & (loc < t.shape[0])
+        t.index_add_(0, loc[ok], g[ok])
         return t
 
     sharded_scatter_add_rows(shard_grad, rb, torch.from_numpy(ids), torch.from_numpy(grads[rank]),
@@ -181,7 +204,7 @@ def _scatter_worker(rank, world, n, d, b, seed):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_scatter_add_rows_gloo(world):
     """Trainable C5 table: row gradients of the global batch summed over ranks
-    and added into their owners' shards (one reduce-scatter by owner segment)."""
+    (one all-reduce) and added by their owners into their shards."""
     _run(world, _scatter_worker, 301, 8, 64, 13)
 
 
@@ -218,9 +241,18 @@ def _c5_worker(rank, world, n, d, b, seed):
         loss.backward()
         return torch.stack([loss.detach(), torch.tensor(0.0), loss.detach()]).double(), uu.grad, pp.grad
 
+    def scatter_add(t, loc, g):
+        ok = (loc >= 0) & (loc < t.shape[0])
+        t.index_add_(0, loc[ok], g[ok])
+        return t
+
     u_loc = torch.from_numpy(users[rank * b:(rank + 1) * b])
+    grad_shard = torch.zeros((cnt, d))
     loss, du, dp = sharded_inbatch_step(shard, beg, u_loc, torch.from_numpy(ids[rank * b:(rank + 1) * b]), 0.1,
-                                        gather=window_gather, loss_fn=cpu_loss)
+                                        gather=window_gather, loss_fn=cpu_loss, grad_shard=grad_shard,
+                                        scatter_add=scatter_add)
+    dp_sum = dp.clone()
+    torch.distributed.all_reduce(dp_sum)  # the frozen path exchanges nothing: sum here to compare
     # equals the single-process reference loss over the whole global batch
     U = torch.from_numpy(users).requires_grad_()
     P = torch.from_numpy(table[ids]).requires_grad_()
@@ -228,7 +260,11 @@ def _c5_worker(rank, world, n, d, b, seed):
     ref.backward()
     np.testing.assert_allclose(float(loss), float(ref), rtol=1e-6)
     np.testing.assert_allclose(du.numpy(), U.grad[rank * b:(rank + 1) * b].numpy(), rtol=1e-5, atol=1e-7)
-    np.testing.assert_allclose(dp.numpy(), P.grad.numpy(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(dp_sum.numpy(), P.grad.numpy(), rtol=1e-5, atol=1e-7)
+    # trainable table: the owners' shard gradients
+    ref_g = np.zeros((n, d), np.float64)
+    np.add.at(ref_g, ids, P.grad.numpy())
+    np.testing.assert_allclose(grad_shard.numpy(), ref_g[beg:beg + cnt], rtol=1e-5, atol=1e-7)
 
 
 def test_sharded_inbatch_step_gloo():

@@ -65,8 +65,8 @@ def test_trainer_resumes_reference_checkpoint(device, golden, tmp_path):
     mine = tr.step.optimizer_state_dict()["state"]
     assert set(mine) == set(ref_ck["optimizer_state"]["state"])
     for i, st in ref_ck["optimizer_state"]["state"].items():
-        assert torch.equal(mine[i]["exp_avg"], st["exp_avg"]), i
-        assert torch.equal(mine[i]["exp_avg_sq"], st["exp_avg_sq"]), i
+        assert torch.equal(mine[i]["exp_avg"].cpu(), st["exp_avg"]), i
+        assert torch.equal(mine[i]["exp_avg_sq"].cpu(), st["exp_avg_sq"]), i
         assert float(mine[i]["step"]) == float(st["step"])
     batch = {k[3:]: torch.from_numpy(v) for k, v in g.items() if k.startswith("b1_")}
     tr.train_loader = [batch]
@@ -92,7 +92,7 @@ def test_trainer_resumes_reference_checkpoint(device, golden, tmp_path):
         assert float(st["step"]) == float(mo[f"step/{i}"]) == 2.0
         for name in ("exp_avg", "exp_avg_sq"):
             ref = mo[f"{name}/{i}"]
-            np.testing.assert_allclose(st[name].numpy(), ref, rtol=1e-4, atol=1e-6 * float(np.abs(ref).max() + 1e-30),
+            np.testing.assert_allclose(st[name].cpu().numpy(), ref, rtol=1e-4, atol=1e-6 * float(np.abs(ref).max() + 1e-30),
                                        err_msg=f"{name}/{i}")
     # and what we write reads back in the same layout (our save -> our resume)
     tr.save_checkpoint(2, is_best=True)

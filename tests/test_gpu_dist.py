@@ -80,3 +80,54 @@ def test_table_window_gather_sums_to_full_gather(device):
     torch.cuda.synchronize()
     assert torch.equal(acc, ref)
     assert torch.equal(ref, table[ids].float())
+
+
+def test_table_window_gather_bytewise_max_is_exact(device):
+    """The exchange of sharded_gather_rows: every window's zero-elsewhere
+    gather combined by a byte-wise max (what the uint8 MAX all-reduce computes
+    across ranks) is the full gather bit for bit, -0.0 included."""
+    rng = np.random.default_rng(3)
+    n, d, world = 1003, 256, 4
+    table = torch.from_numpy(rng.standard_normal((n, d)).astype(np.float32)).to(device, torch.bfloat16)
+    table[::5, 0] = -0.0
+    ids = torch.from_numpy(rng.integers(0, n, size=517)).to(device)
+    acc = torch.zeros((517, d), dtype=torch.bfloat16, device=device)
+    for r in range(world):
+        b, c = shard_range(n, world, r)
+        part = kernels.gather_rows(table[b:b + c], ids, row_begin=b)
+        torch.maximum(acc.view(torch.uint8), part.view(torch.uint8), out=acc.view(torch.uint8))
+    torch.cuda.synchronize()
+    assert torch.equal(acc.view(torch.int16), table[ids].view(torch.int16))
+
+
+def test_c5_sharded_step_captures_in_a_graph(device):
+    """the C5 step has no host synchronisation (the N = 1 path runs
+    the same code as N > 1, collectives aside), so it captures in a hipGraph;
+    replays over new ids equal eager steps bit for bit, and the sync-free id
+    check counts every id."""
+    from rtrec_amd.dist.sharded import sharded_inbatch_step
+    g = torch.Generator(device=device).manual_seed(5)
+    rows, dim, b = 200_000, 256, 1024
+    shard = (torch.randn(rows, dim, device=device, generator=g) * 0.05).to(torch.bfloat16)
+    u = torch.nn.functional.normalize(torch.randn(b, dim, device=device, generator=g), dim=1).to(torch.bfloat16)
+    ids_a = torch.randint(0, rows, (b,), device=device, generator=g)
+    ids_b = torch.randint(0, rows, (b,), device=device, generator=g)
+    status = torch.zeros(2, dtype=torch.int64, device=device)
+    static_ids = ids_a.clone()
+    s = torch.cuda.Stream(device=device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(s):
+        sharded_inbatch_step(shard, 0, u, static_ids, 0.05, status=status)  # warm (workspaces, kernels)
+    torch.cuda.current_stream(device).wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = sharded_inbatch_step(shard, 0, u, static_ids, 0.05, status=status)
+    for ids in (ids_a, ids_b):
+        static_ids.copy_(ids)
+        graph.replay()
+        ref = sharded_inbatch_step(shard, 0, u, ids, 0.05)
+        torch.cuda.synchronize()
+        for a, c in zip(out, ref):
+            assert torch.equal(a, c)
+    torch.cuda.synchronize()
+    assert int(status[0]) == int(status[1]) and int(status[0]) > 0

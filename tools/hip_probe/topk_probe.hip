@@ -36,6 +36,8 @@ static void fill(std::vector<__half>& v, int64_t n, int d, uint64_t seed) {
 
 int main(int argc, char** argv) {
     const int64_t nq = argc > 1 ? atoll(argv[1]) : 65536, nx = argc > 2 ? atoll(argv[2]) : 125000;
+    const int v4mode = argc > 3 ? atoi(argv[3]) : 0;  // rt_flatip_topk_tuning mode (0 auto, 1 old, 2 v4)
+    rt_flatip_topk_tuning(v4mode, 0, -1);
     const int d = 128, reps = 3;
     std::vector<__half> hq(nq * d), hx(nx * d);
     fill(hq, nq, d, 1);
@@ -86,11 +88,12 @@ int main(int argc, char** argv) {
         {
             std::vector<uint64_t> pc(65536 * 6);
             (void)hipMemcpy(pc.data(), rt_topk_probe_cycles_f16(), pc.size() * 8, hipMemcpyDeviceToHost);
-            const int64_t waves = (nq + 255) / 256 * 8;
+            const int64_t waves = v4mode == 2 ? (nq + 511) / 512 * 2 * 8 : (nq + 255) / 256 * 8;
             double acc[6] = {0, 0, 0, 0, 0, 0};
             for (int64_t w = 0; w < waves; ++w)
                 for (int j = 0; j < 6; ++j) acc[j] += static_cast<double>(pc[w * 6 + j]);
-            const char* nm[6] = {"total", "dma-wait", "barrier", "appends", "compaction", "final"};
+            const char* nm[6] = {"total", "dma-wait", "barrier", v4mode == 2 ? "main" : "appends",
+                                 v4mode == 2 ? "sample" : "compaction", v4mode == 2 ? "compact-chk" : "final"};
             printf("   cycles/wave (s_memtime ticks):");
             for (int j = 0; j < 6; ++j) printf(" %s %.0f", nm[j], acc[j] / waves);
             printf("\n");
