@@ -460,11 +460,13 @@ def c5_sharded_step(dev, dist, rank, world, reps=10):
     100M-row x 256 bf16 item table row-sharded 12.5M rows (6.4 GB) per GPU
     (weak scaling: the shard and the per-rank batch stay fixed as N grows, the
     table holds 12.5M·N rows), 8,192 users per rank with uniform global positive
-    ids. One step = the owner-segment row exchange (id all-gather, owners gather
-    their rows, segment all-gather, permutation gather;
-    rtrec_amd/dist/sharded.py::sharded_gather_rows) + the 16-bit in-batch CE
-    forward+backward of the rank's users against ALL gathered rows + the loss and
-    item-gradient all-reduces (sharded_inbatch_step). time = max over ranks."""
+    ids. One step = the sync-free row exchange (id all-gather, every rank
+    gathers the global batch against its own row window, one byte-wise MAX
+    all-reduce of the rows; rtrec_amd/dist/sharded.py::sharded_gather_rows) +
+    the 16-bit in-batch CE forward+backward of the rank's users against ALL
+    gathered rows + the loss all-reduce (sharded_inbatch_step; the table is a
+    frozen feature table as in the reference, so no item-gradient exchange). The
+    same code runs at N = 1 (collectives skipped). time = max over ranks."""
     from rtrec_amd.dist.sharded import sharded_inbatch_step
     rows_per, dim, b, tau = 12_500_000, 256, 8192, 0.05
     g = torch.Generator(device=dev).manual_seed(2000 + rank)
@@ -498,7 +500,8 @@ def c5_sharded_step(dev, dist, rank, world, reps=10):
     out = {"ms_per_step": 1e3 * el / reps, "n_gpus": world, "table_rows": rows_per * world, "shard_rows": rows_per,
            "emb_dim": dim, "users_per_rank": b, "dtype": "bf16", "loss": float(loss[0].item()),
            "pairs_per_s": world * b * (b * world) * reps / el,
-           "exchange": "id all-gather + owner-segment all-gather (+ loss/grad all-reduce)",
+           "exchange": "id all-gather + window gather + byte-wise MAX all-reduce of rows (+ loss all-reduce); "
+                       "no host sync",
            "scaling": "weak (fixed shard and batch per GPU)"}
     del shard
     torch.cuda.empty_cache()

@@ -243,7 +243,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             if (e < TILE_VECS) {
                 const int r = e / (DP / VEC);
                 const int c = e % (DP / VEC);
-                *reinterpret_cast<uint4*>(tile + r * LS + c * VEC) = pre[l];
+                if constexpr (KK == 2) {
+                    // fp32: a row is stored as [even k | odd k] so that the lane
+                    // that feeds k-step s (element 2s + half) reads 4 steps in one
+                    // ds_read_b128 — the natural k order, unchanged, bit-exact
+                    const uint4 v = pre[l];
+                    *reinterpret_cast<uint2*>(tile + r * LS + 2 * c) = make_uint2(v.x, v.z);
+                    *reinterpret_cast<uint2*>(tile + r * LS + DP / 2 + 2 * c) = make_uint2(v.y, v.w);
+                } else {
+                    *reinterpret_cast<uint4*>(tile + r * LS + c * VEC) = pre[l];
+                }
             }
         }
         __syncthreads();
@@ -278,12 +287,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             f32x16 acc[QS];
 #pragma unroll
             for (int j = 0; j < QS; ++j) acc[j] = f32x16{};
-            const T* arow = tile + (rt * 32 + col) * LS + ((KK == 2) ? half : 8 * half);
+            if constexpr (KK == 2) {
+                // k-steps s..s+3 of this lane: 4 consecutive floats of its half
+                const T* arow = tile + (rt * 32 + col) * LS + half * (DP / 2);
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const typename M::frag af = frag_from<T>(arow + s * KK);
+                for (int s = 0; s < S; s += 4) {
+                    const float4 a4 = *reinterpret_cast<const float4*>(arow + s);
 #pragma unroll
-                for (int j = 0; j < QS; ++j) acc[j] = M::run(af, qf[j][s], acc[j]);
+                    for (int j = 0; j < QS; ++j) {
+                        acc[j] = M::run(a4.x, qf[j][s], acc[j]);
+                        acc[j] = M::run(a4.y, qf[j][s + 1], acc[j]);
+                        acc[j] = M::run(a4.z, qf[j][s + 2], acc[j]);
+                        acc[j] = M::run(a4.w, qf[j][s + 3], acc[j]);
+                    }
+                }
+            } else {
+                const T* arow = tile + (rt * 32 + col) * LS + 8 * half;
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const typename M::frag af = frag_from<T>(arow + s * KK);
+#pragma unroll
+                    for (int j = 0; j < QS; ++j) acc[j] = M::run(af, qf[j][s], acc[j]);
+                }
             }
             if (sub0 + 32 > i_end) {  // partial last sub-tile: rows past the end never qualify
                 const int left = static_cast<int>(i_end - sub0);

@@ -294,6 +294,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     const uint32_t wb_hi = static_cast<uint32_t>(
         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase) >> 32)));
     const uint64_t wbase = (static_cast<uint64_t>(wb_hi) << 32) | wb_lo;
+    // wave-uniform global base: the appends compile to SADDR global stores
+    // (a generic pointer would give flat stores, counted in lgkmcnt too)
+    __attribute__((address_space(1))) char* const wbytes =
+        reinterpret_cast<__attribute__((address_space(1))) char*>(wbase);
     uint32_t woff0[QS], woff[QS];
     float thr[QS];
 #pragma unroll
@@ -334,8 +338,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
                     if (r >= rem) off -= static_cast<uint32_t>((r - (rem - 1)) * row_bytes);
                 }
                 unsigned keep;
+                // s_nop 4: the SGPR operands may come straight from a VALU (a spill
+                // reload), which a VMEM read as base needs 5 wait states after
                 asm volatile(
-                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                    "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
                     "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                     : "=&s"(keep)
                     : "v"(off), "s"(sbu), "s"(base + i * (kWavesB * 1024))
@@ -377,15 +383,13 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             bool pass = acc[r] >= t;
             if constexpr (EXCL) pass = pass && !((xw >> tile_row(r, half)) & 1u);
             if (__ballot(pass)) {
-                issued += 2;  // exactly two store instructions for the wave
+                issued += 1;  // exactly one store instruction (dwordx2) for the wave
                 if (pass) {
                     const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
-                    asm volatile(
-                        "global_store_dword %0, %1, %2\n\tglobal_store_dword %0, %3, %2 offset:4\n\t"
-                        "v_add_u32 %0, 8, %0"
-                        : "+v"(wo)
-                        : "v"(acc[r]), "s"(wbase), "v"(id)
-                        : "memory");
+                    // a compiler-visible SADDR store (hipcc counts it and pads its hazards)
+                    *reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(wbytes + wo) =
+                        (static_cast<uint64_t>(id) << 32) | __float_as_uint(acc[r]);
+                    wo += 8;
                 }
             }
         }
