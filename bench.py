@@ -92,6 +92,40 @@ def _host_cores() -> int:
     return len(os.sched_getaffinity(0))
 
 
+def _cgroup_cpu_quota():
+    """CPUs granted by this process's cgroup CPU quota (cgroup v2 cpu.max or v1
+    cfs_quota_us / cfs_period_us), None when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return max(1, -(-q // per)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_cores() -> int:
+    """The cores this process can actually run on: the affinity set, capped by
+    the cgroup CPU quota. On the GPU box the affinity set is the whole 256-core
+    host but the quota is 16 CPUs; torch.set_num_threads(256) there ran one C2
+    step in 30.7 s (profiles/r03s1_bench.json), 16x oversubscribed, against
+    ~90 ms on the 16 granted cores."""
+    q = _cgroup_cpu_quota()
+    if q is None and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        q = int(os.environ["OMP_NUM_THREADS"]) or None  # the box's documented per-job CPU share
+    n = _host_cores()
+    return min(n, q) if q else n
+
+
 # The reference's own C2 step on its CPU path, measured in the survey container
 # (BASELINE.md §2: "Full mixed-loss train step, B=1024, N=16, emb 128, hidden
 # [256,128]: 106 ms", src/training/trainers/two_tower.py:98-146). The only
@@ -105,11 +139,11 @@ def cpu_baseline(host, budget_s=10.0, threads=None):
     """The oracle's torch-CPU restatement of the reference step (same math as
     src/training/trainers/two_tower.py:98-146) on a bounded sample of C2 batches,
     on every core this process may run on (torch.set_num_threads(
-    len(os.sched_getaffinity(0))))."""
+    len(os.sched_getaffinity(0))), capped by the cgroup CPU quota: _cpu_cores)."""
     from oracle import two_tower as orc
     from rtrec_amd.training.utils import create_two_tower_model_for_training
     uf, mf, bu, bp, bn = host
-    threads = threads or _host_cores()
+    threads = threads or _cpu_cores()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     torch.manual_seed(1234)
@@ -133,7 +167,7 @@ def cpu_baseline(host, budget_s=10.0, threads=None):
     pairs = steps * (1024 * 1024 + 1024 * 16)
     torch.set_num_threads(prev)
     return {"value": pairs / el, "unit": "pairs/s", "cores": threads, "threads": threads,
-            "host_cores": _host_cores(), "kind": "port",
+            "host_cores": _host_cores(), "cgroup_cpu_quota": _cgroup_cpu_quota(), "kind": "port",
             "sample": f"{steps} C2 train steps (B=1024, N=16, emb 128) of oracle/two_tower.train_step on "
                       f"torch-CPU with {threads} threads, {el:.1f}s", "ms_per_step": 1000.0 * el / steps}
 
@@ -166,7 +200,7 @@ def cpu_topk_baseline(budget_s=8.0):
     x 128, k=10) and C4 on a query sample (2,048 of the queries against the full
     1M-item corpus, k=100, fp32), QPS extrapolated from the sample; every core
     this process may run on."""
-    threads = _host_cores()
+    threads = _cpu_cores()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(7)
@@ -668,14 +702,11 @@ def main():
                     result["extras"][name] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(host, args.cpu_budget)
-            # the same port on the 16 threads the box's scheduler shares per GPU (labelled leg)
-            try:
-                if _host_cores() > 16:
-                    c16 = cpu_baseline(host, min(args.cpu_budget, 5.0), threads=16)
-                    result["cpu_baseline"]["threads16"] = {k: c16[k] for k in ("value", "threads", "ms_per_step",
-                                                                              "sample")}
-            except Exception as e:
-                result["cpu_baseline"]["threads16"] = {"error": repr(e)}
+            if _cpu_cores() < _host_cores():
+                result["cpu_baseline"]["note"] = (
+                    f"threads = the {_cpu_cores()} CPUs of this process's cgroup quota, not the "
+                    f"{_host_cores()}-core affinity set: {_host_cores()} threads on a {_cpu_cores()}-CPU quota "
+                    "oversubscribe it (r03s1: 30.7 s for one step)")
             try:
                 result["cpu_baseline"]["topk"] = cpu_topk_baseline()
                 ex = result.get("extras", {})
