@@ -172,7 +172,7 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
     if (dtype == RT_F32 || d > 128 || k > v4::kMaxK) return false;
     const bool forced = g_v4_mode == 2;
     if (!forced && (k <= v3::kMaxKv3 || nx < 65536)) return false;
-    constexpr int QT = v4::Geo<2>::QT;
+    constexpr int QT = v4::Geo<v4::kQS>::QT;
     p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
     if (p.chunk < 1) p.chunk = 1;
     p.q_tiles = static_cast<int>((p.chunk + QT - 1) / QT);

@@ -462,7 +462,7 @@ template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
     constexpr bool F32 = sizeof(T) == 4;
     if constexpr (!F32 && S <= 8) {
-        if (p.v4) return v4::launch_S<T, S, 2>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank, a.meta, st);
+        if (p.v4) return v4::launch_S<T, S, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank, a.meta, st);
     }
     if constexpr (F32) {
         switch (list_k(true, a.k)) {

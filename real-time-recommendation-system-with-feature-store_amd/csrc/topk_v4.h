@@ -25,6 +25,11 @@
 //        appends per query (336 at k = 100), against thousands for a running
 //        threshold that starts at -inf. A half nearing its capacity is
 //        compacted by the v2 radix compaction (threshold raised, never lowered).
+//        The filter of a set is a branch-free 16-bit pass mask (two VALU per
+//        score, scheduled into the next set's MFMA gaps) and a wave-uniform
+//        store loop that runs max-popcount times; the block barrier sits
+//        before each stage's last sub-tile so fragments of the next stage are
+//        read behind the current MFMAs (see main_pass).
 //      * verification: a query whose buffer holds >= k entries (all >= thr)
 //        has its split top-k inside it, exactly. A query with fewer (the
 //        estimate overshot) makes the whole block rescan the split for its
@@ -51,6 +56,10 @@ constexpr int kMaxK = 128;
 constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
 constexpr int kMaxSplits = 8;
 constexpr int kFinishCap = 128;        // survivors a finish wave sorts at once (2 per lane)
+#ifndef RT_TOPK_V4_QS
+#define RT_TOPK_V4_QS 2
+#endif
+constexpr int kQS = RT_TOPK_V4_QS;     // query sets of 32 per wave
 
 template <int QS>
 struct Geo {
@@ -125,6 +134,13 @@ __device__ __forceinline__ float union_rank(const float (&l)[kList], int rank) {
 #pragma unroll
     for (int i = 0; i < 2 * kList; ++i) v = (i == rank - 1) ? u[i] : v;
     return v;
+}
+
+// per lane: (bit lane of m) ? b : a, as one v_cndmask_b32
+__device__ __forceinline__ float lane_sel(uint64_t m, float a, float b) {
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
 }
 
 // composite key of a candidate: larger = better (score desc, then id asc)
@@ -363,37 +379,84 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         for (int r = 3; r < 15; r += 2) m = fmaxf(fmaxf(m, acc[r]), acc[r + 1]);
         return fmaxf(m, acc[15]);
     };
-    // Appends of one sub-tile for query set j: row by row, the wave mask of
-    // the lanes whose score passes (one v_cmp into SGPRs); a row no lane
-    // passes is skipped by a scalar branch, otherwise its passing lanes store
-    // (score, id) at their cursors (two SADDR dword stores). With 64
-    // independent queries per wave almost every sub-tile has SOME passing
-    // lane, so this path is the common one: ~16 compares and a few store
-    // blocks, no per-lane loop, no LDS round trip.
-    auto appends = [&](int j, const f32x16& acc, int64_t sub0) {
+    // Appends of one sub-tile for query set j, in two parts so that the
+    // compares never wait on a branch:
+    //  * passmask: the 16 compares fold into a per-lane 16-bit mask (bit r =
+    //    row (r & 3) + 8 (r >> 2) of the lane's half passes) with no branch;
+    //    the caller schedules them into the gaps of the next set's MFMAs.
+    //  * store_loop: a wave-uniform loop that runs max-popcount times (0 or 1
+    //    on almost every sub-tile), each lane storing its lowest passing row
+    //    (the score picked by a 4-level select on that row's bits) with one
+    //    SADDR dwordx2 store at its cursor.
+    // Rows ascend with r, so each lane appends the same entries in the same
+    // order as a row-by-row filter would.
+    auto passmask = [&](int j, const f32x16& acc, int64_t sub0, uint32_t tm) -> uint32_t {
         const float t = thr[j];
-        const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
-        uint32_t xw = 0u;
-        if constexpr (EXCL) {
-            if (excl[j]) xw = excl[j][sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
-        }
-        uint32_t wo = woff[j];
+        uint32_t pm = 0u;
+        // pm = 2 pm + (acc[r] >= t), rows 15..0: two VALU per row, no wait
+        // states (written in C the compiler emits compare, cndmask and or/shift,
+        // with an s_nop between the compare and the cndmask that reads vcc)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            bool pass = acc[r] >= t;
-            if constexpr (EXCL) pass = pass && !((xw >> tile_row(r, half)) & 1u);
-            if (__ballot(pass)) {
-                issued += 1;  // exactly one store instruction (dwordx2) for the wave
-                if (pass) {
-                    const uint32_t id = sub_lane + static_cast<uint32_t>((r & 3) + 8 * (r >> 2));
-                    // a compiler-visible SADDR store (hipcc counts it and pads its hazards)
-                    *reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(wbytes + wo) =
-                        (static_cast<uint64_t>(id) << 32) | __float_as_uint(acc[r]);
-                    wo += 8;
-                }
+        for (int r = 15; r >= 0; --r)
+            asm("v_cmp_ge_f32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                : "+v"(pm)
+                : "v"(acc[r]), "v"(t)
+                : "vcc");
+        pm &= tm;
+        if constexpr (EXCL) {
+            if (excl[j]) {
+                const uint32_t xw = excl[j][sub0 >> 5];  // sub0 is 32-aligned: one bitmap word per sub-tile
+                // this half's rows 4h + {0..3, 8..11, 16..19, 24..27} -> bits r = 0..15
+                const uint32_t xh = xw >> (4 * half);
+                const uint32_t xr = (xh & 0xFu) | ((xh >> 4) & 0xF0u) | ((xh >> 8) & 0xF00u) | ((xh >> 12) & 0xF000u);
+                pm &= ~xr;
+            }
+        }
+        return pm;
+    };
+    auto store_loop = [&](int j, uint32_t pm, const f32x16& acc, int64_t sub0) {
+        const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
+        uint32_t wo = woff[j];
+        while (__ballot(pm != 0u)) {
+            issued += 1;  // exactly one store instruction (dwordx2) for the wave
+            if (pm) {
+                // the lowest passing row as an isolated bit, tested against
+                // constant masks; the score is picked by explicit v_cndmask
+                // instructions (written as selects on acc[], the compiler folds
+                // them into a 16-way variable-index extract of the vector)
+                const uint32_t lb = pm & (0u - pm);
+                pm ^= lb;
+                const bool b0 = (lb & 0xAAAAu) != 0u, b1 = (lb & 0xCCCCu) != 0u;
+                const bool b2 = (lb & 0xF0F0u) != 0u, b3 = (lb & 0xFF00u) != 0u;
+                const uint64_t m0 = __ballot(b0), m1 = __ballot(b1), m2 = __ballot(b2), m3 = __ballot(b3);
+                float v8[8], v4[4], v2[2];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v8[i] = lane_sel(m0, acc[2 * i], acc[2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v4[i] = lane_sel(m1, v8[2 * i], v8[2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 2; ++i) v2[i] = lane_sel(m2, v4[2 * i], v4[2 * i + 1]);
+                const float s = lane_sel(m3, v2[0], v2[1]);
+                const uint32_t id = sub_lane + (b0 ? 1u : 0u) + (b1 ? 2u : 0u) + (b2 ? 8u : 0u) + (b3 ? 16u : 0u);
+                // a compiler-visible SADDR store (hipcc counts it and pads its hazards)
+                *reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(wbytes + wo) =
+                    (static_cast<uint64_t>(id) << 32) | __float_as_uint(s);
+                wo += 8;
             }
         }
         woff[j] = wo;
+    };
+    // rows of a sub-tile with `left` (< 32) valid rows, as this lane's pass-mask bits
+    auto tail_bits = [&](int left) -> uint32_t {
+        const int lim = left - 4 * half;
+        uint32_t m = 0u;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            int c = lim - 8 * g;
+            c = c < 0 ? 0 : (c > 4 ? 4 : c);
+            m |= ((1u << c) - 1u) << (4 * g);
+        }
+        return m;
     };
     // compact every buffer of this wave that may overflow before the next check
     auto maybe_compact = [&]() {
@@ -516,38 +579,99 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         }
     }
 
-    // ---- main pass over every stage (A fragments of sub-tile t+1 read behind t's MFMAs;
-    //      set QS-1 of sub-tile t is filtered during set 0's MFMAs of t+1) ----
+    // ---- main pass over every stage ----
+    // * A fragments of sub-tile t+1 are read behind the MFMAs of t's last set
+    //   (across a stage boundary too), so no LDS read latency is exposed.
+    // * set QS-1 of sub-tile t is filtered behind set 0's MFMAs of t+1.
+    // * the block barrier sits BEFORE a stage's last sub-tile, not between
+    //   stages: there every wave has waited for its own DMA pieces of stage
+    //   v+1 (so after the barrier stage v+1 is visible and the last sub-tile
+    //   can already read its fragments), and every wave is past stage v-1, so
+    //   stage v+2 is DMA'd into that buffer right after it. The DMA has one
+    //   stage to land.
     auto main_pass = [&]() {
         if (nst == 0) return;
-        prologue(nst, false);
+        int mk_next;
+        {
+            fetch(stage_t0(0, false), 0);
+            const int mark0 = issued;
+            if (nst > 1) fetch(stage_t0(1, false), 1);
+            mk_next = issued;
+            wait_vm_le(issued - mark0);
+            raw_barrier();
+        }
         frag af[S];
         f32x16 acc[QS];
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[QS - 1][r] = -INFINITY;  // "previous" of the first sub-tile
+        f32x16 accp = acc[QS - 1];                                 // (QS = 1: the previous sub-tile)
         int64_t sub_prev = i_begin;
+        uint32_t tm_prev = 0u;  // no rows: the first sub-tile has no previous set
         int cur = 0;
         lds_a(af, ring + a_lane, 0);
+        // pins a set's MFMAs above the store loop that follows them (without it the
+        // compiler sinks the MFMAs below the loop, into the block that reads them)
+        auto pin = [&](f32x16& x) { asm volatile("" : "+v"(x)); };
+        // MFMA s of a set, then (optionally) the next sub-tile's fragment s and
+        // 5 VALU (the previous set's compares)
+        auto interleave = [&](bool with_reads, bool with_valu) {
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (with_reads) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (with_valu) __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            }
+        };
         for (int v = 0; v < nst; ++v) {
             const int64_t t0 = stage_t0(v, false);
             const bool more = v + 1 < nst;
             const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);
-            if (v + C::RING - 1 < nst) fetch(stage_t0(v + C::RING - 1, false), cur == 0 ? C::RING - 1 : cur - 1);
-            mk[C::RING - 2] = issued;
             const char* stage = ring + cur * C::TILE_BYTES + a_lane;
-            RT_PT(const uint64_t c0 = clock64();)
+            const char* nstage = ring + (cur == C::RING - 1 ? 0 : cur + 1) * C::TILE_BYTES + a_lane;
+            RT_PT(uint64_t c0 = clock64();)
 #pragma unroll
             for (int rt = 0; rt < C::NSUB; ++rt) {
+                if (rt == C::NSUB - 1) {
+                    RT_PT(const uint64_t c1 = clock64(); pc_main += c1 - c0;)
+                    if (more) wait_vm_le(issued - mk_next);
+                    RT_PT(const uint64_t c2 = clock64(); pc_wait += c2 - c1;)
+                    raw_barrier();
+                    RT_PT(const uint64_t c3 = clock64(); pc_bar += c3 - c2;)
+                    if (more) {
+                        maybe_compact();  // fragments of this sub-tile are live (in registers)
+                        if (v + 2 < nst) fetch(stage_t0(v + 2, false), cur == 0 ? C::RING - 1 : cur - 1);
+                        mk_next = issued;
+                    }
+                    RT_PT(c0 = clock64(); pc_cmp += c0 - c3;)
+                }
                 if (rt * 32 < rem) {
                     const int64_t sub0 = t0 + rt * 32;
-                    // set 0: MFMAs; the previous sub-tile's last set is filtered behind them
+                    // the next sub-tile's rows: this stage, or the next stage's first
+                    // (rows past a partial stage's end are stale but finite, never filtered in)
+                    // (always a valid LDS address: after the last stage the reads are unused)
+                    constexpr bool nxt = true;
+                    const char* nsrc = rt + 1 < C::NSUB ? stage + (rt + 1) * 32 * C::RS : nstage;
+                    uint32_t tm = 0xFFFFu;  // rows past a partial stage's end: masked here
+                    if (rem < (rt + 1) * 32) tm = tail_bits(rem - rt * 32);
+                    // set 0: MFMAs, with the previous sub-tile's last set compared in their gaps
                     acc[0] = f32x16{};
 #pragma unroll
-                    for (int s = 0; s < S; ++s) acc[0] = M::run(af[s], qf[0][s], acc[0]);
-                    if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev);
-                    if (rem < (rt + 1) * 32) mask_tail(acc[0], sub0);
-                    if constexpr (QS == 1) {
-                        if (rt + 1 < C::NSUB) lds_a(af, stage, rt + 1);
+                    for (int s = 0; s < S; ++s) {
+                        acc[0] = M::run(af[s], qf[0][s], acc[0]);
+                        if (QS == 1 && nxt)
+                            af[s] = __builtin_bit_cast(frag, *reinterpret_cast<const uint4*>(nsrc + s * 32));
+                    }
+                    if constexpr (QS > 1) {
+                        const uint32_t pm = passmask(QS - 1, acc[QS - 1], sub_prev, tm_prev);
+                        interleave(false, true);
+                        pin(acc[0]);
+                        store_loop(QS - 1, pm, acc[QS - 1], sub_prev);
+                    } else {  // one set: the previous sub-tile's scores wait in accp
+                        const uint32_t pm = passmask(0, accp, sub_prev, tm_prev);
+                        interleave(nxt, true);
+                        pin(acc[0]);
+                        store_loop(0, pm, accp, sub_prev);
+                        accp = acc[0];
                     }
 #pragma unroll
                     for (int j = 1; j < QS; ++j) {
@@ -555,34 +679,24 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
 #pragma unroll
                         for (int s = 0; s < S; ++s) {
                             acc[j] = M::run(af[s], qf[j][s], acc[j]);
-                            // fragment s is free once its last MFMA issued; rows past a
-                            // partial stage's end are stale but finite and never filtered in
-                            if (j == QS - 1 && rt + 1 < C::NSUB)
-                                af[s] = __builtin_bit_cast(
-                                    frag, *reinterpret_cast<const uint4*>(stage + (rt + 1) * 32 * C::RS + s * 32));
+                            // fragment s is free once its last MFMA issued
+                            if (j == QS - 1 && nxt)
+                                af[s] = __builtin_bit_cast(frag, *reinterpret_cast<const uint4*>(nsrc + s * 32));
                         }
-                        appends(j - 1, acc[j - 1], sub0);
-                        if (rem < (rt + 1) * 32) mask_tail(acc[j], sub0);
+                        const uint32_t pm = passmask(j - 1, acc[j - 1], sub0, tm);
+                        interleave(j == QS - 1 && nxt, true);
+                        pin(acc[j]);
+                        store_loop(j - 1, pm, acc[j - 1], sub0);
                     }
-                    if constexpr (QS == 1) appends(0, acc[0], sub0);
                     sub_prev = sub0;
+                    tm_prev = tm;
                 }
             }
-            RT_PT(const uint64_t c1 = clock64(); pc_main += c1 - c0;)
-            if (more) wait_vm_le(issued - mk[0]);
-            RT_PT(const uint64_t c2 = clock64(); pc_wait += c2 - c1;)
-            raw_barrier();
-            RT_PT(const uint64_t c3 = clock64(); pc_bar += c3 - c2;)
-#pragma unroll
-            for (int i = 0; i + 1 < C::RING - 1; ++i) mk[i] = mk[i + 1];
+            RT_PT(pc_main += clock64() - c0;)
             cur = cur == C::RING - 1 ? 0 : cur + 1;
-            if (more) {
-                maybe_compact();  // the only check in the loop: between stages, before any fragment is live
-                RT_PT(pc_cmp += clock64() - c3;)
-                lds_a(af, ring + cur * C::TILE_BYTES + a_lane, 0);
-            }
         }
-        if constexpr (QS > 1) appends(QS - 1, acc[QS - 1], sub_prev);
+        if constexpr (QS > 1) store_loop(QS - 1, passmask(QS - 1, acc[QS - 1], sub_prev, tm_prev), acc[QS - 1], sub_prev);
+        else store_loop(0, passmask(0, accp, sub_prev, tm_prev), accp, sub_prev);
         maybe_compact();
     };
 #ifdef RT_TOPK_PROBE_NOSEL
