@@ -56,6 +56,7 @@ constexpr int kMaxK = 128;
 constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
 constexpr int kMaxSplits = 8;
 constexpr int kFinishCap = 128;        // survivors a finish wave sorts at once (2 per lane)
+constexpr int kFinishRegs = 16;        // candidates per lane the finish holds in registers
 #ifndef RT_TOPK_V4_QS
 #define RT_TOPK_V4_QS 2
 #endif
@@ -150,7 +151,7 @@ __device__ __forceinline__ uint64_t ckey(const Cand& c) {
 __device__ __forceinline__ uint64_t prefix_mask(int shift) { return shift >= 64 ? 0ull : (~0ull << shift); }
 
 // Radix select over candidates visited by each(fn) (whole wave calls; fn gets
-// every entry exactly once, on some lane): 8 bits of the composite key a pass,
+// every entry's composite key exactly once, on some lane): 8 bits of the composite key a pass,
 // from the top, until the entries whose key's top (64 - shift) bits are >=
 // prefix's number <= limit. That set always holds the k best entries (k <=
 // limit). Registers: a few; LDS: hist (256 words, this wave's).
@@ -164,8 +165,7 @@ __device__ __forceinline__ void radix_prefix(Each&& each, int k, int limit, uint
         reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_sync();
         const uint64_t pmask = prefix_mask(shift), pre = prefix;
-        each([&](const Cand& c) {
-            const uint64_t key = ckey(c);
+        each([&](uint64_t key) {
             if ((key & pmask) == pre) atomicAdd(&hist[(key >> sh) & 255u], 1u);
         });
         wave_lds_sync();
@@ -214,8 +214,8 @@ __device__ __forceinline__ void compact_stream(Cand* __restrict__ buf, int& n0, 
     __threadfence_block();
     const int a0 = n0, a1 = n1;
     auto each = [&](auto&& fn) {
-        for (int i = lane; i < a0; i += 64) fn(buf[i]);
-        for (int i = lane; i < a1; i += 64) fn(buf[kHalf + i]);
+        for (int i = lane; i < a0; i += 64) fn(ckey(buf[i]));
+        for (int i = lane; i < a1; i += 64) fn(ckey(buf[kHalf + i]));
     };
     uint64_t prefix = 0;
     int shift = 64, kept = a0 + a1;
@@ -808,13 +808,74 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
         for (int sg = 0; sg < nseg; ++sg) {
             const int n = __shfl(cnt, sg, 64);
             const Cand* p = seg_ptr(sg);
-            for (int i = lane; i < n; i += 64) fn(p[i]);
+            for (int i = lane; i < n; i += 64) fn(ckey(p[i]));
         }
     };
     float* os = out_s + q * k;
     int64_t* oi = out_i + q * k;
 
-    // radix select on the composite key until <= kFinishCap entries remain
+    if (total <= 64 * kFinishRegs) {
+        // Register path (the C4 shapes: ~700 candidates): every candidate is
+        // read ONCE, as its composite key, into this lane's slots f = e*64 + lane
+        // of the segments' concatenation. The radix select then starts below
+        // the bits all keys share (scores above one threshold agree in sign,
+        // exponent and the top mantissa bits), so its first pass already
+        // splits them, and no pass re-reads memory.
+        int bnd[2 * kMaxSplits];  // inclusive segment ends (wave-uniform)
+#pragma unroll
+        for (int t = 0; t < 2 * kMaxSplits; ++t) bnd[t] = __builtin_amdgcn_readlane(pre, t);
+        uint64_t key[kFinishRegs];
+        uint64_t mx = 0ull, mn = ~0ull;
+#pragma unroll
+        for (int e = 0; e < kFinishRegs; ++e) {
+            const int f = e * 64 + lane;
+            key[e] = 0ull;
+            if (f < total) {
+                int sg = 0, base = 0;
+#pragma unroll
+                for (int t = 0; t + 1 < 2 * kMaxSplits; ++t)
+                    if (t + 1 < nseg && f >= bnd[t]) { sg = t + 1; base = bnd[t]; }
+                key[e] = ckey(seg_ptr(sg)[f - base]);
+                mx = key[e] > mx ? key[e] : mx;
+                mn = key[e] < mn ? key[e] : mn;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a = __shfl_xor(mx, o, 64), b = __shfl_xor(mn, o, 64);
+            mx = a > mx ? a : mx;
+            mn = b < mn ? b : mn;
+        }
+        int shift = 64 - (mx == mn ? 64 : __builtin_clzll(mx ^ mn));  // bits below the shared prefix
+        if (shift < 8) shift = 8;
+        uint64_t prefix = mx & prefix_mask(shift);
+        int kept = total;
+        auto eachr = [&](auto&& fn) {
+#pragma unroll
+            for (int e = 0; e < kFinishRegs; ++e)
+                if (e * 64 + lane < total) fn(key[e]);
+        };
+        if (total > kFinishCap) radix_prefix(eachr, k, kFinishCap, hist, prefix, shift, kept);
+        const uint64_t pmask = prefix_mask(shift);
+        int m = 0;
+#pragma unroll
+        for (int e = 0; e < kFinishRegs; ++e) {
+            const bool take = e * 64 + lane < total && (key[e] & pmask) >= prefix;
+            const uint64_t bm = __ballot(take);
+            const int pos = m + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                    static_cast<uint32_t>(bm >> 32),
+                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bm), 0u)));
+            if (take && pos < kFinishCap)
+                keep[pos] = Cand{v2::okey_inv(static_cast<uint32_t>(key[e] >> 32)), ~static_cast<uint32_t>(key[e])};
+            m += __popcll(bm);
+        }
+        if (m > kFinishCap) m = kFinishCap;  // cannot happen: the prefix bounds it
+        wave_lds_sync();
+        finish_sort<2>(keep, m, k, os, oi, id_offset);
+        return;
+    }
+
+    // streaming path: radix select on the composite key until <= kFinishCap entries remain
     uint64_t prefix = 0;
     int shift = 64, kept = total;
     if (total > kFinishCap) radix_prefix(each, k, kFinishCap, hist, prefix, shift, kept);
