@@ -242,13 +242,17 @@ def topk_extras(dev):
     for _ in range(3):
         kernels.flatip_topk(q, x, 10)
     torch.cuda.synchronize()
-    TIMER.enable(["flatip_topk"])
+    # wall clock of back-to-back calls (QPS), then the kernel timer's pass
+    # (its GPU spin ahead of each launch must not count in the QPS)
     reps = 20
     t0 = time.perf_counter()
     for _ in range(reps):
         kernels.flatip_topk(q, x, 10)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
+    TIMER.enable(["flatip_topk"])
+    for _ in range(reps):
+        kernels.flatip_topk(q, x, 10)
     s = TIMER.summary()["flatip_topk"]
     TIMER.disable()
     out["topk_c3"] = {"qps": 6040 / el, "ms": el * 1e3, "kernel_ms": s["avg_ms"],
@@ -259,18 +263,21 @@ def topk_extras(dev):
     x = torch.nn.functional.normalize(torch.randn(125000, 128, device=dev, generator=g), dim=1).half()
     kernels.flatip_topk(q, x, 100)
     torch.cuda.synchronize()
-    TIMER.enable(["flatip_topk"])
     reps = 3
     t0 = time.perf_counter()
     for _ in range(reps):
         kernels.flatip_topk(q, x, 100)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
+    TIMER.enable(["flatip_topk"])
+    for _ in range(reps):
+        kernels.flatip_topk(q, x, 100)
     s = TIMER.summary()["flatip_topk"]
     TIMER.disable()
     tf = s["flops"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e12
-    out["topk_c4_shard"] = {"qps": 65536 / el, "ms": el * 1e3, "tflops": tf, "mfma_frac": tf / PEAK_BF16_TFLOPS,
-                            "dtype": "f16", "k": 100, "shape": "65536x125000x128"}
+    out["topk_c4_shard"] = {"qps": 65536 / el, "ms": el * 1e3, "kernel_ms": s["avg_ms"], "tflops": tf,
+                            "mfma_frac": tf / PEAK_BF16_TFLOPS, "dtype": "f16", "k": 100,
+                            "shape": "65536x125000x128"}
     del q, x
     # config 5 gather: bf16 rows of 256 from a 12.5M-row shard, 16M ids per launch
     rows = 12_500_000

@@ -826,16 +826,28 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
         for (int t = 0; t < 2 * kMaxSplits; ++t) bnd[t] = __builtin_amdgcn_readlane(pre, t);
         uint64_t key[kFinishRegs];
         uint64_t mx = 0ull, mn = ~0ull;
+        // all loads issued before any is used; the segment of slot f found by
+        // a search over NS - 1 boundaries (NS = 4: the 2-split C4 plans)
+        auto load_all = [&](auto ns_tag) {
+            constexpr int NS = decltype(ns_tag)::value;
+#pragma unroll
+            for (int e = 0; e < kFinishRegs; ++e) {
+                const int f = e * 64 + lane;
+                key[e] = 0ull;
+                if (f < total) {
+                    int sg = 0, base = 0;
+#pragma unroll
+                    for (int t = 0; t + 1 < NS; ++t)
+                        if (t + 1 < nseg && f >= bnd[t]) { sg = t + 1; base = bnd[t]; }
+                    key[e] = ckey(seg_ptr(sg)[f - base]);
+                }
+            }
+        };
+        if (nseg <= 4) load_all(std::integral_constant<int, 4>{});
+        else load_all(std::integral_constant<int, 2 * kMaxSplits>{});
 #pragma unroll
         for (int e = 0; e < kFinishRegs; ++e) {
-            const int f = e * 64 + lane;
-            key[e] = 0ull;
-            if (f < total) {
-                int sg = 0, base = 0;
-#pragma unroll
-                for (int t = 0; t + 1 < 2 * kMaxSplits; ++t)
-                    if (t + 1 < nseg && f >= bnd[t]) { sg = t + 1; base = bnd[t]; }
-                key[e] = ckey(seg_ptr(sg)[f - base]);
+            if (e * 64 + lane < total) {
                 mx = key[e] > mx ? key[e] : mx;
                 mn = key[e] < mn ? key[e] : mn;
             }
