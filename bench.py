@@ -263,17 +263,19 @@ def topk_extras(dev):
     x = torch.nn.functional.normalize(torch.randn(125000, 128, device=dev, generator=g), dim=1).half()
     kernels.flatip_topk(q, x, 100)
     torch.cuda.synchronize()
-    reps = 3
+    # kernel-timer pass first (it also brings the clocks up), then the wall clock
+    # of back-to-back calls for the QPS
+    reps = 10
+    TIMER.enable(["flatip_topk"])
+    for _ in range(3):
+        kernels.flatip_topk(q, x, 100)
+    s = TIMER.summary()["flatip_topk"]
+    TIMER.disable()
     t0 = time.perf_counter()
     for _ in range(reps):
         kernels.flatip_topk(q, x, 100)
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
-    TIMER.enable(["flatip_topk"])
-    for _ in range(reps):
-        kernels.flatip_topk(q, x, 100)
-    s = TIMER.summary()["flatip_topk"]
-    TIMER.disable()
     tf = s["flops"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e12
     out["topk_c4_shard"] = {"qps": 65536 / el, "ms": el * 1e3, "kernel_ms": s["avg_ms"], "tflops": tf,
                             "mfma_frac": tf / PEAK_BF16_TFLOPS, "dtype": "f16", "k": 100,
