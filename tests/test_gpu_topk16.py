@@ -167,3 +167,29 @@ def test_topk16_v4_massive_ties_and_exclusion(K, V4):
     _check(K, q, x, 100, torch.float16, exclude=excl, id_offset=7_000_000)
     V4()
     _check(K, q, x, 64, torch.bfloat16, exclude=excl)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_topk16_v4_full_query_chunk_vs_v2(K, dtype):
+    """A full 65,536-query chunk (the C4 query count; v4 forced below its
+    65,536-row corpus bound): compared bit for bit with the v2 kernel on the
+    same inputs (both exact), with an exclusion bitmap, an id offset and a
+    ragged last stage."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    nq, nx, d, k = 65536, 20011, 128, 100
+    q = (torch.randint(-64, 65, (nq, d), device="cuda", generator=g) / 64).to(dtype)
+    x = (torch.randint(-64, 65, (nx, d), device="cuda", generator=g) / 64).to(dtype)
+    words = (nx + 31) // 32
+    bits = torch.randint(-2**31, 2**31 - 1, (nq, words), device="cuda", generator=g, dtype=torch.int64)
+    bits = (bits & torch.randint(-2**31, 2**31 - 1, (nq, words), device="cuda", generator=g, dtype=torch.int64))
+    bits = (bits & 0x11111111).to(torch.int32)  # ~1 in 16 items excluded per query
+    try:
+        K.topk_tuning(1, 0, -1)  # v2 / v3 only
+        rs, ri = K.flatip_topk(q, x, k, exclude_bits=bits, id_offset=123_456)
+        K.topk_tuning(2, 0, -1)  # v4 (forced below its 65,536-row bound)
+        gs, gi = K.flatip_topk(q, x, k, exclude_bits=bits, id_offset=123_456)
+        torch.cuda.synchronize()
+    finally:
+        K.topk_tuning(0, 0, -1)
+    assert torch.equal(gi, ri)
+    assert torch.equal(gs, rs)
