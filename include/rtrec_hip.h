@@ -95,7 +95,8 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
 /* Planner override of rt_flatip_topk (tests and tuning; process-wide, not
  * thread-safe, results unchanged by any setting). v4_mode: 0 automatic, 1 never
  * the sampled-threshold kernel pair, 2 it wherever legal (16-bit, d <= 128,
- * k <= 128). v4_stride: sample every stride-th 128-row stage (0 = planner).
+ * k <= 128); + 4: per-split thresholds instead of one corpus-wide threshold
+ * per query when the items are split. v4_stride: sample every stride-th 128-row stage (0 = planner).
  * v4_rank: threshold = rank-th largest sampled group maximum (-1 = planner,
  * 0 = no sample: a running threshold from -inf). Set before sizing the
  * workspace. */

@@ -122,6 +122,7 @@ constexpr int64_t kCUs = 256;  // MI355X compute units
 static int g_v4_mode = 0;     // 0 auto, 1 never, 2 wherever legal
 static int g_v4_stride = 0;   // 0: planner's choice
 static int g_v4_rank = -1;    // -1: planner's choice; 0: no sample (v2-style running threshold)
+static int g_v4_joint = 1;    // 1: over several splits, one corpus-wide threshold per query
 
 // log P(Bin(n, f) >= r)
 inline double log_binom_tail(int n, double f, int r) {
@@ -188,12 +189,17 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
     p.splits = static_cast<int>(nx > 0 ? (nx + p.items_per_split - 1) / p.items_per_split : 1);
     p.cap = v4::kCap;
     p.v4 = 1;
-    plan_v4_sample(k, p.items_per_split, p.stride, p.rank);
+    // several splits: one threshold per query from a sample of the whole corpus
+    // (the union of the splits' buffers then holds ~rank*stride entries, not
+    // splits times that); one split: the per-split form
+    p.v4_joint = (p.splits > 1 && g_v4_joint) ? 1 : 0;
+    plan_v4_sample(k, p.v4_joint ? nx : p.items_per_split, p.stride, p.rank);
     if (g_v4_stride > 0) p.stride = g_v4_stride;
     if (g_v4_rank >= 0) p.rank = g_v4_rank;
     const int64_t q_pad = static_cast<int64_t>(p.q_tiles) * QT;
     p.cand_bytes = static_cast<size_t>(p.splits) * q_pad * v4::kCap * sizeof(Cand);
     p.meta_bytes = static_cast<size_t>(p.splits) * q_pad * 2 * sizeof(int);
+    p.fail_bytes = p.v4_joint ? static_cast<size_t>(q_pad) * sizeof(int) : 0;
     p.part_bytes = 0;
     return true;
 }
@@ -244,7 +250,7 @@ extern "C" size_t rt_flatip_topk_workspace_bytes(int64_t nq, int64_t nx, int d, 
     if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return 256;
     const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
     return topk::align256(p.cand_bytes) + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes) +
-           256;
+           topk::align256(p.fail_bytes) + 256;
 }
 
 extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
@@ -263,12 +269,14 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
     const size_t cand_al = topk::align256(p.cand_bytes);
     if (!workspace ||
-        workspace_bytes < cand_al + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes))
+        workspace_bytes < cand_al + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes) +
+                              topk::align256(p.fail_bytes))
         return RT_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
     char* part = reinterpret_cast<char*>(workspace) + cand_al;
     int* meta = reinterpret_cast<int*>(part + p.part_bytes);
     uint32_t* kth = reinterpret_cast<uint32_t*>(part + p.part_bytes + topk::align256(p.meta_bytes));
+    int* fail = reinterpret_cast<int*>(part + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes));
     const size_t esz = dtype == RT_F32 ? 4 : 2;
     for (int64_t q0 = 0; q0 < nq; q0 += p.chunk) {
         const int64_t nc = (nq - q0) < p.chunk ? (nq - q0) : p.chunk;
@@ -292,6 +300,7 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
         a.cand = reinterpret_cast<Cand*>(workspace);
         a.id_offset = id_offset;
         a.meta = meta;
+        a.fail = fail;
         if (p.kth_bytes) {
             a.kth_shared = kth;
             const hipError_t e = hipMemsetAsync(kth, 0, static_cast<size_t>(nc) * sizeof(uint32_t), st);
@@ -322,8 +331,11 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
 }
 
 extern "C" int rt_flatip_topk_tuning(int v4_mode, int v4_stride, int v4_rank) {
-    if (v4_mode < 0 || v4_mode > 2 || v4_stride < 0 || v4_rank < -1 || v4_rank > 2 * topk::v4::kList)
+    if (v4_mode < 0 || (v4_mode & 3) > 2 || v4_mode > 6 || v4_stride < 0 || v4_rank < -1 ||
+        v4_rank > 2 * topk::v4::kList)
         return RT_ERR_INVALID;
+    topk::g_v4_joint = (v4_mode & 4) ? 0 : 1;
+    v4_mode &= 3;
     topk::g_v4_mode = v4_mode;
     topk::g_v4_stride = v4_stride;
     topk::g_v4_rank = v4_rank;

@@ -99,6 +99,8 @@ struct Plan {
     int cap;             // candidate buffer entries per query (v1 kernel), else 0
     size_t cand_bytes, part_bytes;
     int v4;              // 1: the sampled-threshold scan + finish pair (topk_v4.h)
+    int v4_joint;        // v4 over > 1 split: one threshold per query from a corpus-wide sample
+    size_t fail_bytes;   // v4 joint: per-query flags (union of the split buffers < k)
     int stride, rank;    // v4 sample: every stride-th stage; threshold = rank-th group maximum
     size_t meta_bytes;   // v4 per-(split, query, half) entry counts
     size_t kth_bytes;    // register-list kernel over > 1 split: the shared per-query k-th keys
@@ -109,6 +111,7 @@ struct Args {
     const uint32_t* excl; int64_t excl_words;
     Cand* cand; float* out_s; int64_t* out_i; int64_t id_offset;
     int* meta;
+    int* fail;             // v4 joint threshold: per-query rescue flags (nullptr: per-split mode)
     uint32_t* kth_shared;  // register-list kernel, split corpora: per query, the best split k-th score (okey)
 };
 
@@ -462,7 +465,9 @@ template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
     constexpr bool F32 = sizeof(T) == 4;
     if constexpr (!F32 && S <= 8) {
-        if (p.v4) return v4::launch_S<T, S, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank, a.meta, st);
+        if (p.v4)
+            return v4::launch_S<T, S, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank, a.meta,
+                                               p.v4_joint ? a.fail : nullptr, st);
     }
     if constexpr (F32) {
         switch (list_k(true, a.k)) {

@@ -252,7 +252,8 @@ __device__ __forceinline__ void compact_stream(Cand* __restrict__ buf, int& n0, 
 
 template <typename T, int S, int QS, bool EXCL>
 __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, int64_t items_per_split, int stride,
-                                                            int rank, int* __restrict__ meta) {
+                                                            int rank, int* __restrict__ meta, int mode,
+                                                            const int* __restrict__ fail) {
     using M = Mfma<T>;
     using C = Cfg4<T, S>;
     typedef typename M::frag frag;
@@ -277,7 +278,16 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32·QS buffers
     uint32_t* const whist = hist_all + wave * 256;
     const int nst = i_end > i_begin ? static_cast<int>((i_end - i_begin + C::NT - 1) / C::NT) : 0;
-    const int nsa = (rank > 0 && stride > 0) ? (nst + stride - 1) / stride : 0;  // sample stages
+    // mode 0: per-split sample, per-split verification (rescan on failure);
+    // mode 1 (joint): the sample pass covers the WHOLE corpus, so every split of
+    //   a query derives the same threshold, a lower bound of the query's k-th
+    //   over the corpus; no per-split verification (the finish checks the union);
+    // mode 2 (rescue): only queries the finish flagged (union < k) run, from -inf.
+    const bool joint = mode == 1;
+    // rows [p_begin, p_end) of the current pass (fetch, tail masks, stages)
+    int64_t p_begin = joint ? 0 : i_begin, p_end = joint ? a.nx : i_end;
+    const int nst_s = joint ? static_cast<int>((a.nx + C::NT - 1) / C::NT) : nst;
+    const int nsa = (mode != 2 && rank > 0 && stride > 0) ? (nst_s + stride - 1) / stride : 0;  // sample stages
     if (tid == 0) *flag = 0u;
 
     frag qf[QS][S];
@@ -322,6 +332,21 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         woff[j] = woff0[j];
         thr[j] = qok[j] ? -FLT_MAX : INFINITY;
     }
+    if (mode == 2) {  // rescue: the flagged queries from -inf (a running threshold), the rest skip
+        __syncthreads();  // *flag zeroed above
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < QS; ++j) {
+            const bool f = qok[j] && fail[qw + j * 32 + col] != 0;
+            thr[j] = f ? -FLT_MAX : INFINITY;
+            any |= f;
+        }
+        if (__ballot(any) != 0 && lane == 0) atomicOr(flag, 1u);
+        __syncthreads();
+        if (*flag == 0u) return;  // block-uniform: no flagged query here (the common case)
+        __syncthreads();          // every wave has read the flag before it is reused below
+        if (tid == 0) *flag = 0u;
+    }
     constexpr int kHead = C::NSUB * 16;  // appends per half between two compaction checks, at most
     constexpr uint32_t kLimBytes = static_cast<uint32_t>((kHalf - kHead) * sizeof(Cand));
     constexpr int kLimit = kHalf - kHead;  // a compaction keeps at most this many entries (in all)
@@ -344,7 +369,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     auto fetch = [&](int64_t t0, int buf) {
         const uint32_t base = ring0 + buf * C::TILE_BYTES + wave_u * 1024;
         const uint64_t sbu = reinterpret_cast<uint64_t>(Xb + t0 * row_bytes);
-        const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);
+        const int rem = static_cast<int>(p_end - t0 < C::NT ? p_end - t0 : C::NT);
 #pragma unroll
         for (int i = 0; i < C::MAXP; ++i) {
             if (i < npieces) {
@@ -490,7 +515,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             af[s] = __builtin_bit_cast(frag, *reinterpret_cast<const uint4*>(stage + rt * 32 * C::RS + s * 32));
     };
     auto mask_tail = [&](f32x16& acc, int64_t sub0) {
-        const int left = static_cast<int>(i_end - sub0);
+        const int left = static_cast<int>(p_end - sub0);
         if (left < 32) {
 #pragma unroll
             for (int r = 0; r < 16; ++r)
@@ -511,7 +536,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     // stage v of a pass: rows [stage_row(v), +NT); `sample` passes visit every
     // stride-th stage
     auto stage_t0 = [&](int v, bool sample) -> int64_t {
-        return i_begin + static_cast<int64_t>(sample ? v * stride : v) * C::NT;
+        return p_begin + static_cast<int64_t>(sample ? v * stride : v) * C::NT;
     };
 
     // ---- sample pass: group-max lists ----
@@ -540,7 +565,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         for (int v = 0; v < nsa; ++v) {
             const int64_t t0 = stage_t0(v, true);
             const bool more = v + 1 < nsa;
-            const int rem = static_cast<int>(i_end - t0 < C::NT ? i_end - t0 : C::NT);
+            const int rem = static_cast<int>(p_end - t0 < C::NT ? p_end - t0 : C::NT);
             if (v + C::RING - 1 < nsa) fetch(stage_t0(v + C::RING - 1, true), cur == 0 ? C::RING - 1 : cur - 1);
             mk[C::RING - 2] = issued;
             const char* stage = ring + cur * C::TILE_BYTES + a_lane;
@@ -578,6 +603,8 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             if (qok[j]) thr[j] = e > -FLT_MAX ? e : -FLT_MAX;
         }
     }
+    p_begin = i_begin;  // the main pass covers this block's split
+    p_end = i_end;
 
     // ---- main pass over every stage ----
     // * A fragments of sub-tile t+1 are read behind the MFMAs of t's last set
@@ -709,7 +736,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
 #ifdef RT_TOPK_PROBE_NOSEL
     if (false) {
 #else
-    if (nsa > 0) {
+    if (mode == 0 && nsa > 0) {
 #endif
         bool any = false;
 #pragma unroll
@@ -781,12 +808,13 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
                                                              const int* __restrict__ meta, int splits,
                                                              int64_t q_pad, int64_t nq, int k,
                                                              float* __restrict__ out_s, int64_t* __restrict__ out_i,
-                                                             int64_t id_offset) {
+                                                             int64_t id_offset, int mode, int* __restrict__ fail) {
     __shared__ __attribute__((aligned(16))) uint32_t hist_all[4][256];
     __shared__ __attribute__((aligned(16))) Cand keep_all[4][kFinishCap];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + w;
     if (q >= nq) return;
+    if (mode == 2 && fail[q] == 0) return;
     uint32_t* hist = hist_all[w];
     Cand* keep = keep_all[w];
     const int nseg = 2 * splits;
@@ -800,6 +828,14 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
         if (lane >= o) pre += t;
     }
     const int total = __shfl(pre, 63, 64);
+    // mode 1 (joint threshold): the union of the split buffers must hold k
+    // entries, else the query is flagged for the rescue pair of launches;
+    // mode 2: only the flagged queries (their buffers rebuilt from -inf)
+    if (mode == 1) {
+        const bool short_ = total < k;
+        if (lane == 0) fail[q] = short_ ? 1 : 0;
+        if (short_) return;
+    }
     auto seg_ptr = [&](int sg) {
         return cand + ((static_cast<int64_t>(sg >> 1) * q_pad) + q) * kCap + (sg & 1) * kHalf;
     };
@@ -920,20 +956,28 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
 
 template <typename T, int S, int QS>
 int launch_S(const Args& a, int q_tiles, int splits, int64_t items_per_split, int stride, int rank, int* meta,
-             hipStream_t st) {
-    dim3 grid(static_cast<unsigned>(q_tiles * splits));
-    if (a.excl)
-        hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, true>), grid, dim3(64 * kWavesB), 0, st, a, splits,
-                           items_per_split, stride, rank, meta);
-    else
-        hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, false>), grid, dim3(64 * kWavesB), 0, st, a, splits,
-                           items_per_split, stride, rank, meta);
-    int rc = check_launch("flatip_topk_v4_scan");
-    if (rc) return rc;
+             int* fail, hipStream_t st) {
+    // joint threshold (several splits): scan + finish, then the rescue pair,
+    // whose blocks exit at once unless the finish flagged one of their queries
+    const int passes = fail ? 2 : 1;
     const int64_t q_pad = static_cast<int64_t>(q_tiles) * Geo<QS>::QT;
-    hipLaunchKernelGGL(flatip_topk_v4_finish<4>, dim3(static_cast<unsigned>((a.nq + 3) / 4)), dim3(256), 0, st, a.cand,
-                       meta, splits, q_pad, a.nq, a.k, a.out_s, a.out_i, a.id_offset);
-    return check_launch("flatip_topk_v4_finish");
+    for (int pass = 0; pass < passes; ++pass) {
+        const int mode = fail ? 1 + pass : 0;
+        dim3 grid(static_cast<unsigned>(q_tiles * splits));
+        if (a.excl)
+            hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, true>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                               items_per_split, stride, rank, meta, mode, fail);
+        else
+            hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, false>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                               items_per_split, stride, rank, meta, mode, fail);
+        int rc = check_launch("flatip_topk_v4_scan");
+        if (rc) return rc;
+        hipLaunchKernelGGL(flatip_topk_v4_finish<4>, dim3(static_cast<unsigned>((a.nq + 3) / 4)), dim3(256), 0, st,
+                           a.cand, meta, splits, q_pad, a.nq, a.k, a.out_s, a.out_i, a.id_offset, mode, fail);
+        rc = check_launch("flatip_topk_v4_finish");
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 }  // namespace v4
