@@ -149,6 +149,12 @@ inline double log_binom_tail(int n, double f, int r) {
 // overshoots the split's k-th score (a rescan) with probability <= 1e-6 —
 // P(>= rank of the split's top k fall in the sample) for a 1/f sample; the
 // group-maximum estimate sits at or below the item rank, so this bounds it.
+#ifndef RT_TOPK_V4_APPEND_CAP
+#define RT_TOPK_V4_APPEND_CAP 960.0
+#endif
+// (stride, rank) of the v4 sample over `items_per_split` rows: the largest
+// stride whose failure-safe rank keeps the expected appends (rank * stride,
+// per query) within RT_TOPK_V4_APPEND_CAP
 inline void plan_v4_sample(int k, int64_t items_per_split, int& stride, int& rank) {
     const int64_t nst = (items_per_split + v4::Cfg4<__half, 8>::NT - 1) / v4::Cfg4<__half, 8>::NT;
     stride = 0;
@@ -159,7 +165,7 @@ inline void plan_v4_sample(int k, int64_t items_per_split, int& stride, int& ran
         const double f = static_cast<double>(nsa) / static_cast<double>(nst);
         for (int r = 1; r <= 2 * v4::kList; ++r) {
             if (log_binom_tail(k, f, r) <= std::log(1e-6)) {
-                if (r / f <= 360.0) { stride = st; rank = r; return; }
+                if (r / f <= RT_TOPK_V4_APPEND_CAP) { stride = st; rank = r; return; }
                 break;
             }
         }
