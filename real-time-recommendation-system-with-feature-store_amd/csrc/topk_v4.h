@@ -35,6 +35,12 @@
 //        estimate overshot) makes the whole block rescan the split for its
 //        failed queries with thr = -inf and the compaction path of v2 —
 //        correct for any data, costly only when it happens.
+//      * joint mode (mode 1, several splits): the sample pass covers the
+//        whole corpus, so every split of a query derives the same threshold,
+//        a lower bound of its corpus-wide k-th; the finish checks the union
+//        of the split buffers instead (< k entries: the query is flagged),
+//        and a rescue launch pair (mode 2) rebuilds the flagged queries from
+//        -inf while every other block exits at once.
 //    Each (split, query, half) writes its entry count to `meta`.
 // 2. flatip_topk_v4_finish: one wave per query over the union of its split
 //    buffers: a radix select on the composite key (order-preserving score
