@@ -152,6 +152,9 @@ inline double log_binom_tail(int n, double f, int r) {
 #ifndef RT_TOPK_V4_APPEND_CAP
 #define RT_TOPK_V4_APPEND_CAP 960.0
 #endif
+#ifndef RT_TOPK_V4_MAX_STRIDE
+#define RT_TOPK_V4_MAX_STRIDE 64
+#endif
 // (stride, rank) of the v4 sample over `items_per_split` rows: the largest
 // stride whose failure-safe rank keeps the expected appends (rank * stride,
 // per query) within RT_TOPK_V4_APPEND_CAP
@@ -159,7 +162,7 @@ inline void plan_v4_sample(int k, int64_t items_per_split, int& stride, int& ran
     const int64_t nst = (items_per_split + v4::Cfg4<__half, 8>::NT - 1) / v4::Cfg4<__half, 8>::NT;
     stride = 0;
     rank = 0;
-    for (int st = 64; st >= 2; --st) {
+    for (int st = RT_TOPK_V4_MAX_STRIDE; st >= 2; --st) {
         const int64_t nsa = (nst + st - 1) / st;
         if (nsa < 4) continue;  // fewer than 32 groups per query in the sample
         const double f = static_cast<double>(nsa) / static_cast<double>(nst);
