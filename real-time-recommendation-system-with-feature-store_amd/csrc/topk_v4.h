@@ -17,12 +17,13 @@
 //        a sorted register list, one v_med3 per level per insert, no ids.
 //      * the estimate: thr = the `rank`-th largest of the query's 32 group
 //        maxima (both lane halves). The host picks (stride, rank) so that
-//        P(thr > the split's k-th score) = P(Bin(k, 1/stride) >= rank) is
-//        below 1e-6 (topk_api.hip::plan_v4).
+//        P(thr > the k-th score) = P(Bin(k, f) >= rank) is below 1e-6 for
+//        the sampled fraction f, with rank / f (the expected appends) at
+//        most RT_TOPK_V4_APPEND_CAP (topk_api.hip::plan_v4_sample).
 //      * main phase: every stage (the sample stages again), each score >= thr
 //        appended to the query's candidate buffer (per lane half: one
-//        SADDR 8-byte store at the lane's cursor). About rank * stride
-//        appends per query (336 at k = 100), against thousands for a running
+//        SADDR 8-byte store at the lane's cursor). About rank / f appends
+//        per query (~600 at the C4 shapes), against thousands for a running
 //        threshold that starts at -inf. A half nearing its capacity is
 //        compacted by the v2 radix compaction (threshold raised, never lowered).
 //        The filter of a set is a branch-free 16-bit pass mask (two VALU per
@@ -295,6 +296,20 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     const int nst_s = joint ? static_cast<int>((a.nx + C::NT - 1) / C::NT) : nst;
     const int nsa = (mode != 2 && rank > 0 && stride > 0) ? (nst_s + stride - 1) / stride : 0;  // sample stages
     if (tid == 0) *flag = 0u;
+    if (mode == 2) {  // rescue: exit before any load unless a query of this block was flagged
+        __syncthreads();  // *flag zeroed above
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < QS; ++j) {
+            const int64_t q = qw + j * 32 + col;
+            any |= q < nq && fail[q] != 0;
+        }
+        if (__ballot(any) != 0 && lane == 0) atomicOr(flag, 1u);
+        __syncthreads();
+        if (*flag == 0u) return;  // block-uniform (the common case: nothing flagged)
+        __syncthreads();          // every wave has read the flag before it is reused below
+        if (tid == 0) *flag = 0u;
+    }
 
     frag qf[QS][S];
     bool qok[QS];
@@ -339,19 +354,8 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         thr[j] = qok[j] ? -FLT_MAX : INFINITY;
     }
     if (mode == 2) {  // rescue: the flagged queries from -inf (a running threshold), the rest skip
-        __syncthreads();  // *flag zeroed above
-        bool any = false;
 #pragma unroll
-        for (int j = 0; j < QS; ++j) {
-            const bool f = qok[j] && fail[qw + j * 32 + col] != 0;
-            thr[j] = f ? -FLT_MAX : INFINITY;
-            any |= f;
-        }
-        if (__ballot(any) != 0 && lane == 0) atomicOr(flag, 1u);
-        __syncthreads();
-        if (*flag == 0u) return;  // block-uniform: no flagged query here (the common case)
-        __syncthreads();          // every wave has read the flag before it is reused below
-        if (tid == 0) *flag = 0u;
+        for (int j = 0; j < QS; ++j) thr[j] = (qok[j] && fail[qw + j * 32 + col] != 0) ? -FLT_MAX : INFINITY;
     }
     constexpr int kHead = C::NSUB * 16;  // appends per half between two compaction checks, at most
     constexpr uint32_t kLimBytes = static_cast<uint32_t>((kHalf - kHead) * sizeof(Cand));
