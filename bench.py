@@ -674,7 +674,8 @@ def main():
         "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "vs_baseline_source": (
             f"BASELINE.md §2: the reference's own CPU C2 step, {BASELINE_MD_C2_MS:g} ms = "
-            f"{BASELINE_MD_C2_PAIRS_PER_S / 1e6:.2f} M pairs/s (survey container, 8 ATen threads)"),
+            f"{BASELINE_MD_C2_PAIRS_PER_S / 1e6:.2f} M pairs/s (survey container, 8 ATen threads; a different "
+            f"machine from this run: vs_cpu_baseline_same_box divides by cpu_baseline.value measured here)"),
         "dtype": "f32",
         "data": "synthetic ML-1M-shaped (6040 users x 3416 movies, seeded; ratings.dat unavailable)",
         "config": {"workload": "C2: MovieLens-1M two-tower train step, emb 128, batch 1024, 16 negatives, "
@@ -711,6 +712,10 @@ def main():
                     result["extras"][name] = {"error": repr(e)}
         if not args.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(host, args.cpu_budget)
+            # two ratios, two machines: vs_baseline (the headline field) divides by
+            # BASELINE.md's reference step timed in the survey container; this one
+            # divides by the oracle step timed on THIS box's host cores in this run
+            result["vs_cpu_baseline_same_box"] = value / result["cpu_baseline"]["value"]
             if _cpu_cores() < _host_cores():
                 result["cpu_baseline"]["note"] = (
                     f"threads = the {_cpu_cores()} CPUs of this process's cgroup quota, not the "

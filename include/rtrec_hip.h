@@ -114,10 +114,16 @@ int rt_flatip_topk_tuning(int v4_mode, int v4_stride, int v4_rank);
  * asc, id asc), into scores/ids [nq, k]; unfilled slots (FLT_MAX, -1). The
  * selection score and the reported distance round differently: exact (equal to
  * Faiss) unless more than k_sel - k items lie within rounding of the k-th
- * distance. k_sel <= 512; sel_ids may alias ids only when k_sel == k. */
+ * distance. With sel_scores ([nq, k_sel], the selection scores rt_flatip_topk
+ * returned with sel_ids) and unverified (int32 [nq]) both given, the finish
+ * certifies each query: unverified[q] = 0 when no unselected item can reach
+ * the k-th distance within a rounding bound, 1 otherwise (the caller then
+ * re-selects that query with a larger k_sel). k_sel <= 512; sel_ids may alias
+ * ids only when k_sel == k. */
 int rt_l2_augment_f32(const float* x, int64_t n, int d, float* out, int ld_out, int role, void* stream);
 int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq, int k_sel,
-                     const int64_t* sel_ids, int k, float* scores, int64_t* ids, int64_t id_offset, void* stream);
+                     const int64_t* sel_ids, const float* sel_scores, int k, float* scores, int64_t* ids,
+                     int32_t* unverified, int64_t id_offset, void* stream);
 
 /* Merge n_lists candidate lists per query, layout [n_lists][nq][k_in] (as an
  * all_gather_into_tensor over ranks produces), into the (score desc, id asc)

@@ -13,9 +13,13 @@
 // re-sorts by (distance asc, id asc) — Faiss's max-heap keeps the lower id on
 // exact ties — and keeps the k best. The augmented score and the reported
 // distance round differently, so items can swap order near the k-th distance;
-// the k_sel − k extra candidates (32 in kernels.flatl2_topk) absorb that: the
-// result is Faiss's unless more than k_sel − k items sit within rounding of the
-// k-th distance. Unfilled slots: (FLT_MAX, −1).
+// the k_sel − k extra candidates (32 in kernels.flatl2_topk) absorb that, and
+// the finish CERTIFIES each query: with the selection scores passed in, a
+// query is flagged (unverified[q] = 1) unless the k-th reported distance sits
+// below ‖q‖² − 2·s_last (s_last = the k_sel-th selection score, the best any
+// unselected item can have) by more than a rounding bound of both quantities;
+// the host re-selects flagged queries with a wider k_sel. Unfilled slots:
+// (FLT_MAX, −1).
 #include <float.h>
 
 #include "rt_common.h"
@@ -51,9 +55,10 @@ constexpr int kFinishN = 512;  // entries per wave (k <= 512)
 // one wave per query: exact distances of the k_sel candidates, re-sorted, k kept
 __global__ __launch_bounds__(256) void finish_kernel(const float* __restrict__ q_aug, int ld_q,
                                                      const float* __restrict__ x_aug, int ld_x, int d, int64_t nq,
-                                                     int k_sel, const int64_t* __restrict__ sel_ids, int k,
+                                                     int k_sel, const int64_t* __restrict__ sel_ids,
+                                                     const float* __restrict__ sel_scores, int k,
                                                      float* __restrict__ scores, int64_t* __restrict__ ids,
-                                                     int64_t id_offset) {
+                                                     int32_t* __restrict__ unverified, int64_t id_offset) {
     __shared__ Cand buf[4][kFinishN];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + w;
@@ -86,6 +91,28 @@ __global__ __launch_bounds__(256) void finish_kernel(const float* __restrict__ q
         scores[q * k + e] = ok ? -c.s : FLT_MAX;
         ids[q * k + e] = ok ? static_cast<int64_t>(c.i) + id_offset : -1;
     }
+    if (unverified && lane == 0) {
+        // certificate: an unselected item y has selection score ŝ_y <= s_last, so
+        // its distance ‖q‖² − 2·s_y is at least qn − 2·s_last minus the rounding of
+        // the selection score and of the reported distance. An item that can
+        // compete with the k-th distance has ‖x‖ ≈ ‖q‖, so every term is bounded
+        // by scale = 2·qn + 2|s_last| + d_k; the bound allows (d + 4) roundings
+        // of that scale, 8x over. A short selection (the whole eligible corpus
+        // was selected) needs no certificate.
+        int flag = 0;
+        if (sel_scores && k_sel > k && sel_ids[q * k_sel + k_sel - 1] >= 0) {
+            const float s_last = sel_scores[q * k_sel + k_sel - 1];
+            const Cand ck = b[k - 1];
+            const float d_k = ck.i != kEmptyId ? -ck.s : FLT_MAX;
+            const float gap = (qn - 2.f * s_last) - d_k;
+            const float scale = 2.f * qn + 2.f * fabsf(s_last) + d_k;
+            const float tol = 8.f * static_cast<float>(d + 4) * 1.1920929e-07f * scale;
+            flag = !(gap > tol);
+        } else if (k_sel == k && sel_ids[q * k_sel + k_sel - 1] >= 0) {
+            flag = 1;  // no over-selection and a full list: nothing certifies the k-th
+        }
+        unverified[q] = flag;
+    }
 }
 
 }  // namespace l2
@@ -103,14 +130,15 @@ extern "C" int rt_l2_augment_f32(const float* x, int64_t n, int d, float* out, i
 }
 
 extern "C" int rt_l2_finish_f32(const float* q_aug, int ld_q, const float* x_aug, int ld_x, int d, int64_t nq,
-                                int k_sel, const int64_t* sel_ids, int k, float* scores, int64_t* ids,
-                                int64_t id_offset, void* stream) {
+                                int k_sel, const int64_t* sel_ids, const float* sel_scores, int k, float* scores,
+                                int64_t* ids, int32_t* unverified, int64_t id_offset, void* stream) {
     if (nq < 0 || d <= 0 || k <= 0 || k_sel < k || ld_q < d || ld_x < d || id_offset < 0) return RT_ERR_INVALID;
     if (k_sel > l2::kFinishN) return RT_ERR_UNSUPPORTED;
     if (nq == 0) return RT_OK;
     if (!q_aug || !x_aug || !sel_ids || !scores || !ids) return RT_ERR_INVALID;
     if (sel_ids == ids && k_sel != k) return RT_ERR_INVALID;  // in place only without over-selection
     hipLaunchKernelGGL(l2::finish_kernel, dim3(static_cast<unsigned>((nq + 3) / 4)), dim3(256), 0, as_stream(stream),
-                       q_aug, ld_q, x_aug, ld_x, d, nq, k_sel, sel_ids, k, scores, ids, id_offset);
+                       q_aug, ld_q, x_aug, ld_x, d, nq, k_sel, sel_ids, sel_scores, k, scores, ids, unverified,
+                       id_offset);
     return check_launch("l2_finish_kernel");
 }

@@ -129,37 +129,38 @@ def _exchange_rows(local: torch.Tensor, group) -> torch.Tensor:
     (exactly one owner per valid position): the max over ranks of the raw BYTES
     (non-owners contribute 0x00) is the owner's row bit for bit — including
     -0.0 and NaN payloads, which a float sum would not preserve. One all-reduce
-    (uint8 MAX; RCCL ncclUint8), no host synchronisation."""
-    flat = local.contiguous().view(torch.uint8)
-    dist.all_reduce(flat, op=dist.ReduceOp.MAX, group=group)
-    return local
+    (uint8 MAX; RCCL ncclUint8), no host synchronisation. Returns the reduced
+    buffer (a contiguous copy when ``local`` was not contiguous)."""
+    buf = local.contiguous()
+    dist.all_reduce(buf.view(torch.uint8), op=dist.ReduceOp.MAX, group=group)
+    return buf
 
 
-def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Tensor, group=None,
-                        gather: Optional[Callable] = None, counts: Optional[Sequence[int]] = None,
-                        status: Optional[torch.Tensor] = None, check: bool = False,
-                        return_ids: bool = False):
-    """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL
-    batch (all ranks' ``ids`` concatenated in rank order) on every rank.
+def _batch_counts(ids: torch.Tensor, counts: Optional[Sequence[int]], uniform: bool, group,
+                  world: int, rank: int) -> Optional[list]:
+    """Per-rank batch sizes: the caller's ``counts``; None when every rank holds
+    the same number of ids (``uniform``, or one rank); otherwise one all-gather
+    of the sizes (a device→host read: ragged batches without ``counts`` cannot
+    be graph-captured)."""
+    if counts is not None:
+        counts = [int(c) for c in counts]
+        if len(counts) != world:
+            raise ValueError(f"counts has {len(counts)} entries for {world} ranks")
+        if ids.numel() != counts[rank]:
+            raise ValueError(f"rank {rank} holds {ids.numel()} ids, counts say {counts[rank]}")
+        return counts
+    if uniform or world == 1:
+        return None
+    mine = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
+    sizes = torch.empty(world, dtype=torch.int64, device=ids.device)
+    dist.all_gather_into_tensor(sizes, mine, group=group)
+    return [int(c) for c in sizes.tolist()]
 
-    Sync-free, graph-capturable exchange (no device→host read anywhere):
-    one all-gather of the batch ids (each rank's ids padded to the batch width
-    with -1); every rank gathers the WHOLE global batch against its own row
-    window (``rt_gather_rows`` with ``row_begin``: ids outside the window, and
-    the -1 padding, give zero rows and are counted as out-of-window); one
-    all-reduce of the rows' bytes (:func:`_exchange_rows`) leaves every
-    position holding its owner's row. Rows are copied, never summed, so the
-    result is bit-identical to a single-table gather.
 
-    ``counts``: per-rank batch sizes when they differ (host data, e.g. the last
-    ragged batch); by default every rank's batch has this rank's size (the C5
-    step). ``status`` (int64 [2], device, optional): accumulates (positions,
-    positions owned by some rank); they differ iff some id lies outside every
-    window — the id-range check without a sync. ``check=True`` reads it and
-    raises IndexError (one sync). ``gather(table, ids, row_begin)`` returns
-    [len(ids), dim] with zero rows outside the window, as ``rt_gather_rows``
-    does (the default). ``return_ids``: also return the global ids (-1 padding
-    removed)."""
+def _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform):
+    """Shared body of :func:`sharded_gather_rows`: (rows of the global batch,
+    global ids, this rank's count of positions it owns (int64 [1], device, NOT
+    reduced over ranks), number of valid positions)."""
     gather_fn = gather
     oob = None
     if gather_fn is None:
@@ -167,9 +168,8 @@ def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Te
         gather_fn = lambda t, i, b: kernels.gather_rows(t, i, row_begin=b, oob=oob)  # noqa: E731
     world, rank = _world(group)
     ids = ids.to(torch.int64)
+    counts = _batch_counts(ids, counts, uniform, group, world, rank)
     width = max(counts) if counts is not None else ids.numel()
-    if counts is not None and ids.numel() != counts[rank]:
-        raise ValueError(f"rank {rank} holds {ids.numel()} ids, counts say {counts[rank]}")
     if world > 1:
         padded = ids
         if ids.numel() != width:
@@ -181,32 +181,73 @@ def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Te
         all_ids = ids
     rows = gather_fn(table_shard, all_ids, row_begin)
     n_valid = sum(counts) if counts is not None else world * width
-    if status is not None or check:
-        if oob is not None:
-            owned = all_ids.numel() - oob.to(torch.int64)
-        else:
-            loc = all_ids - int(row_begin)
-            owned = ((loc >= 0) & (loc < table_shard.shape[0])).sum().reshape(1)
-        if world > 1:
-            dist.all_reduce(owned, op=dist.ReduceOp.SUM, group=group)
-        # (no host→device copy: capturable) positions, positions owned by some rank
-        st = torch.cat([torch.full((1,), n_valid, dtype=torch.int64, device=ids.device), owned])
-        if status is not None:
-            status += st
-        if check and int(st[0]) != int(st[1]):
-            raise IndexError("batch id outside every rank's table window")
+    if oob is not None:
+        owned = all_ids.numel() - oob.to(torch.int64)
+    else:
+        loc = all_ids - int(row_begin)
+        owned = ((loc >= 0) & (loc < table_shard.shape[0])).sum().reshape(1)
     if world > 1:
         rows = _exchange_rows(rows, group)
     if counts is not None and any(c != width for c in counts):  # drop the padding (host-known positions)
         keep = torch.cat([torch.arange(r * width, r * width + c, device=ids.device) for r, c in enumerate(counts)])
         rows = rows.index_select(0, keep)
         all_ids = all_ids.index_select(0, keep)
+    return rows, all_ids, owned, n_valid
+
+
+def _status_update(status: Optional[torch.Tensor], check: bool, n_valid: int, owned_total: torch.Tensor):
+    """(positions, positions owned by some rank) added to ``status``; they
+    differ iff some id lies outside every window. ``check`` reads them (sync)."""
+    st = torch.cat([torch.full((1,), n_valid, dtype=torch.int64, device=owned_total.device),
+                    owned_total.reshape(1).to(torch.int64)])
+    if status is not None:
+        status += st.to(status.device)
+    if check and int(st[0]) != int(st[1]):
+        raise IndexError("batch id outside every rank's table window")
+
+
+def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Tensor, group=None,
+                        gather: Optional[Callable] = None, counts: Optional[Sequence[int]] = None,
+                        status: Optional[torch.Tensor] = None, check: bool = False,
+                        return_ids: bool = False, uniform: bool = False):
+    """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL
+    batch (all ranks' ``ids`` concatenated in rank order) on every rank.
+
+    One all-gather of the batch ids (each rank's ids padded to the batch width
+    with -1); every rank gathers the WHOLE global batch against its own row
+    window (``rt_gather_rows`` with ``row_begin``: ids outside the window, and
+    the -1 padding, give zero rows and are counted as out-of-window); one
+    all-reduce of the rows' bytes (:func:`_exchange_rows`) leaves every
+    position holding its owner's row. Rows are copied, never summed, so the
+    result is bit-identical to a single-table gather.
+
+    Batch sizes: ``counts`` (host data, one entry per rank) when the caller
+    knows them; ``uniform=True`` when every rank holds the same number of ids
+    (the C5 step) — then no device→host read happens anywhere and the call can
+    be captured in a hipGraph; otherwise the sizes are all-gathered first (one
+    tiny collective and a host read), so ragged batches always work.
+
+    Id-range check: the positions owned by some rank are counted on the device
+    and summed over ranks by one 8-byte all-reduce that EVERY rank runs
+    (whatever ``status``/``check`` it passes, so mismatched arguments cannot
+    deadlock). ``status`` (int64 [2], device, optional) accumulates
+    (positions, owned positions); they differ iff some id lies outside every
+    window. ``check=True`` reads them and raises IndexError (one sync).
+    ``gather(table, ids, row_begin)`` returns [len(ids), dim] with zero rows
+    outside the window, as ``rt_gather_rows`` does (the default).
+    ``return_ids``: also return the global ids (-1 padding removed)."""
+    world, _ = _world(group)
+    rows, all_ids, owned, n_valid = _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform)
+    if world > 1:
+        dist.all_reduce(owned, op=dist.ReduceOp.SUM, group=group)
+    _status_update(status, check, n_valid, owned)
     return (rows, all_ids) if return_ids else rows
 
 
 def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_ids: torch.Tensor,
                              grad_rows: torch.Tensor, group=None,
-                             scatter_add: Optional[Callable] = None) -> torch.Tensor:
+                             scatter_add: Optional[Callable] = None,
+                             status: Optional[torch.Tensor] = None, check: bool = False) -> torch.Tensor:
     """Backward of :func:`sharded_gather_rows` for a TRAINABLE row-sharded table
     (the nn.Embedding path a2 under C5 sharding, SURVEY §8(e) "next"): every rank
     holds its own contribution to d loss / d rows for the whole global batch
@@ -214,16 +255,42 @@ def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_id
     of each row adds the sum over ranks into its shard's gradient
     (``grad_shard`` [rows, D], shard rows start at global ``row_begin``).
 
-    Sync-free: one all-reduce (sum) of the row gradients, then every rank
+    Sync-free: one all-reduce (sum, fp32) of the row gradients, then every rank
     scatter-adds the rows of its own window (``rt_scatter_add_rows_f32`` skips
-    ids outside [0, rows); repeated ids accumulate)."""
+    ids outside [0, rows); repeated ids accumulate). The all-reduce moves
+    2(N-1)/N · B_total·D·4 bytes per rank; an owner reduce-scatter moves half
+    that but needs the per-owner counts on the host (a sync) or fixed padded
+    owner segments of B_total rows each (N/2 times MORE bytes), so the
+    all-reduce is the sync-free optimum here.
+
+    Id-range check without an extra collective: this rank's count of ids inside
+    its window rides in one extra row of the same all-reduce (exact in fp32 for
+    B_total < 2^24), so the sum is the number of positions owned by some rank.
+    ``status`` (int64 [2]) accumulates (positions, owned positions); ``check``
+    raises IndexError when they differ (one sync)."""
     scatter_add = scatter_add or (lambda t, ids, g: kernels.scatter_add_rows(t, ids, g))
     world, _ = _world(group)
-    g = grad_rows
-    if world > 1:
-        g = grad_rows.contiguous().clone()
-        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-    return scatter_add(grad_shard, global_ids.to(torch.int64) - int(row_begin), g)
+    gids = global_ids.to(torch.int64)
+    loc = gids - int(row_begin)
+    n_pos = gids.numel()
+    track = status is not None or check
+    if track and n_pos >= (1 << 24):
+        raise ValueError("status/check count positions in fp32: B_total must be < 2^24")
+    d = grad_rows.shape[-1]
+    if world > 1 or track:
+        g = torch.zeros((n_pos + 1, d), dtype=torch.float32, device=grad_rows.device)
+        g[:n_pos] = grad_rows.reshape(n_pos, d)
+        g[n_pos, 0] = ((loc >= 0) & (loc < grad_shard.shape[0])).sum().to(torch.float32)
+        if world > 1:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+        owned = g[n_pos, 0].round().to(torch.int64)
+        g = g[:n_pos]
+    else:
+        g = grad_rows
+        owned = None
+    if track:
+        _status_update(status, check, n_pos, owned)
+    return scatter_add(grad_shard, loc, g)
 
 
 def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: torch.Tensor,
@@ -234,10 +301,13 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     """Config C5 data-parallel in-batch step (SURVEY §8(e) training): the item
     table is row-sharded, every rank holds ``user_emb`` [b, D] for its own b
     users and ``item_ids`` [b] of their positives (b equal on every rank). The
-    global batch's item rows come from :func:`sharded_gather_rows` (sync-free);
-    each rank scores its users against ALL gathered items (label of local user
-    i = global item rank·b + i) with ``rt_inbatch_loss_fwd_bwd``; the loss is
-    averaged over ranks (one 8-byte all-reduce).
+    global batch's item rows come from the sync-free exchange of
+    :func:`sharded_gather_rows` (``uniform``: equal batches); each rank scores
+    its users against ALL gathered items (label of local user i = global item
+    rank·b + i) with ``rt_inbatch_loss_fwd_bwd``; the loss is averaged over
+    ranks by one 16-byte all-reduce that also carries the owned-position
+    count of the id-range check (``status``), so the step runs exactly three
+    collectives: ids all-gather, row MAX all-reduce, (loss, owned) all-reduce.
 
     The item table is a frozen feature table in the reference
     (src/training/datasets/movielens.py:61-63,116), so by default the item-row
@@ -250,13 +320,15 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     (this rank's part))."""
     world, rank = _world(group)
     b = user_emb.shape[0]
-    rows, gids = sharded_gather_rows(table_shard, row_begin, item_ids, group, gather, status=status,
-                                     return_ids=True)
+    rows, gids, owned, n_valid = _gather_global(table_shard, row_begin, item_ids, group, gather, None, True)
     loss_fn = loss_fn or (lambda u, p, off: kernels.inbatch_loss(u, p, temperature, label_offset=off))
     loss, du, dp = loss_fn(user_emb, rows, rank * b)
-    lv = loss[0:1].clone()
+    red = torch.cat([loss[0:1].to(torch.float64), owned.to(torch.float64).reshape(1).to(loss.device)])
     if world > 1:
-        dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=group)
+    lv = red[0:1]
+    if status is not None:
+        _status_update(status, False, n_valid, red[1].round().to(torch.int64))
     if grad_shard is not None:
         sharded_scatter_add_rows(grad_shard, row_begin, gids, dp.float() / world, group, scatter_add)
     # each rank's loss is a mean over its own b users; the global mean averages them

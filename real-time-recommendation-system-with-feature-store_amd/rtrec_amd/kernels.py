@@ -149,22 +149,56 @@ def l2_augment(x: torch.Tensor, role: int, out: Optional[torch.Tensor] = None) -
 
 
 def flatl2_topk(q_aug: torch.Tensor, x_aug: torch.Tensor, d: int, k: int,
-                exclude_bits: Optional[torch.Tensor] = None, id_offset: int = 0
+                exclude_bits: Optional[torch.Tensor] = None, id_offset: int = 0, verify: bool = True
                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact squared-L2 k-NN on augmented rows (IndexFlatL2.search): (distances
     [nq, k] ascending, ids [nq, k]); unfilled slots (FLT_MAX, -1). k + 32
     candidates are selected on the augmented inner product and re-ranked on
-    Faiss's distance (rt_l2_finish_f32)."""
+    Faiss's distance (rt_l2_finish_f32), which certifies every query: a query
+    whose k-th distance is within a rounding bound of what an unselected item
+    could reach (near-duplicate or clustered corpora) is re-selected with 512
+    candidates. ``verify`` costs one device→host read (the flagged count);
+    ``L2_STATS`` counts re-selected queries and any left uncertified (only
+    possible when more than 512 - k items tie within rounding of the k-th)."""
+    nq, nx = q_aug.shape[0], x_aug.shape[0]
     k_sel = min(k + L2_MARGIN, 512)
-    _, sel = flatip_topk(q_aug, x_aug, k_sel, exclude_bits=exclude_bits, id_offset=id_offset)
-    s = torch.empty((q_aug.shape[0], k), dtype=torch.float32, device=q_aug.device)
-    i = torch.empty((q_aug.shape[0], k), dtype=torch.int64, device=q_aug.device)
-    call("rt_l2_finish_f32", ptr(q_aug), q_aug.shape[1], ptr(x_aug), x_aug.shape[1], d, q_aug.shape[0], k_sel,
-         ptr(sel), k, ptr(s), ptr(i), id_offset, stream_of(q_aug))
+    s = torch.empty((nq, k), dtype=torch.float32, device=q_aug.device)
+    i = torch.empty((nq, k), dtype=torch.int64, device=q_aug.device)
+    if nq == 0:
+        return s, i
+    verify = verify and k_sel < nx  # a selection of the whole corpus is exact by construction
+    flags = torch.empty(nq, dtype=torch.int32, device=q_aug.device) if verify else None
+
+    def select_finish(q, bits, ksel, out_s, out_i, out_f):
+        sel_s, sel = flatip_topk(q, x_aug, ksel, exclude_bits=bits, id_offset=id_offset)
+        call("rt_l2_finish_f32", ptr(q), q.shape[1], ptr(x_aug), x_aug.shape[1], d, q.shape[0], ksel,
+             ptr(sel), ptr(sel_s) if out_f is not None else None, k, ptr(out_s), ptr(out_i), ptr(out_f),
+             id_offset, stream_of(q))
+
+    select_finish(q_aug, exclude_bits, k_sel, s, i, flags)
+    if verify:
+        bad = torch.nonzero(flags).flatten()
+        nb = bad.numel()
+        left = 0
+        if nb and k_sel < min(512, nx):
+            qb = q_aug.index_select(0, bad).contiguous()
+            bb = exclude_bits.index_select(0, bad).contiguous() if exclude_bits is not None else None
+            s2 = torch.empty((nb, k), dtype=torch.float32, device=q_aug.device)
+            i2 = torch.empty((nb, k), dtype=torch.int64, device=q_aug.device)
+            f2 = torch.empty(nb, dtype=torch.int32, device=q_aug.device)
+            select_finish(qb, bb, min(512, nx), s2, i2, f2)
+            s.index_copy_(0, bad, s2)
+            i.index_copy_(0, bad, i2)
+            left = int(f2.sum().item())
+        elif nb:
+            left = nb
+        L2_STATS["reselected"] += nb if k_sel < min(512, nx) else 0
+        L2_STATS["uncertified"] += left
     return s, i
 
 
 L2_MARGIN = 32  # over-selected candidates per query in the L2 mode
+L2_STATS = {"reselected": 0, "uncertified": 0}  # flatl2_topk certificate outcomes (process-wide)
 
 
 def topk_merge(scores: torch.Tensor, ids: torch.Tensor, k_out: int

@@ -100,7 +100,7 @@ SIGNATURES = {
     "rt_clip_adam_step": (c_int, [vp, vp, vp, vp, c_i64, vp, c_int, c_f32, c_f32, vp, c_f32, c_f32, c_f32,
                                   c_f32, c_int, vp, vp, c_i64, vp]),
     "rt_l2_augment_f32": (c_int, [vp, c_i64, c_int, vp, c_int, c_int, vp]),
-    "rt_l2_finish_f32": (c_int, [vp, c_int, vp, c_int, c_int, c_i64, c_int, vp, c_int, vp, vp, c_i64, vp]),
+    "rt_l2_finish_f32": (c_int, [vp, c_int, vp, c_int, c_int, c_i64, c_int, vp, vp, c_int, vp, vp, vp, c_i64, vp]),
     "rt_exclusion_bitmap": (c_int, [vp, vp, c_i64, vp, c_i64, c_i64, vp, c_i64, vp]),
     "rt_rank_metrics": (c_int, [vp, c_i64, c_int, vp, vp, vp, c_i64, vp, vp, vp, c_i64, vp, c_int, c_i64, vp, vp,
                                 vp, vp]),

@@ -169,6 +169,25 @@ def _gather_worker(rank, world, n, d, seed, counts, skew):
     with pytest.raises(IndexError):  # every rank with ids planted one bad id
         sharded_gather_rows(shard, b, bad, gather=window_gather, counts=counts if len(set(counts)) > 1 else None,
                             check=True)
+    # ragged batches WITHOUT counts: the sizes are all-gathered (no hang, same rows)
+    rows3 = sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=window_gather)
+    np.testing.assert_array_equal(rows3.numpy(), ref)
+    # ranks passing different status/check arguments: the owned-count all-reduce
+    # runs on every rank regardless, so nothing deadlocks
+    st2 = torch.zeros(2, dtype=torch.int64)
+    sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=window_gather,
+                        status=st2 if rank == 0 else None)
+    if rank == 0:
+        assert st2[0] == st2[1] == sum(counts)
+
+    # a gather that returns a NON-contiguous tensor: the exchanged rows are kept
+    def strided_gather(t, ids, begin):
+        out = window_gather(t, ids, begin)
+        wide = torch.zeros((out.shape[1], out.shape[0]), dtype=out.dtype)
+        wide.copy_(out.t())
+        return wide.t()  # same values, column-major storage
+    rows4 = sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=strided_gather)
+    np.testing.assert_array_equal(rows4.numpy(), ref)
 
 
 @pytest.mark.parametrize("world,counts,skew", [(2, [13, 29], False), (4, [7, 0, 31, 16], False),
@@ -196,9 +215,21 @@ def _scatter_worker(rank, world, n, d, b, seed):
         t.index_add_(0, loc[ok], g[ok])
         return t
 
+    status = torch.zeros(2, dtype=torch.int64)
     sharded_scatter_add_rows(shard_grad, rb, torch.from_numpy(ids), torch.from_numpy(grads[rank]),
-                             scatter_add=scatter_add)
+                             scatter_add=scatter_add, status=status)
     np.testing.assert_allclose(shard_grad.numpy(), ref[rb:rb + rc], rtol=1e-5, atol=1e-5)
+    assert status[0] == status[1] == b
+    # an id outside every window is counted (sync-free) and raised with check=True
+    bad = torch.from_numpy(ids).clone()
+    bad[1] = n + 3
+    st = torch.zeros(2, dtype=torch.int64)
+    sharded_scatter_add_rows(torch.zeros((rc, d)), rb, bad, torch.from_numpy(grads[rank]),
+                             scatter_add=scatter_add, status=st)
+    assert int(st[0]) == b and int(st[1]) == b - 1
+    with pytest.raises(IndexError):
+        sharded_scatter_add_rows(torch.zeros((rc, d)), rb, bad, torch.from_numpy(grads[rank]),
+                                 scatter_add=scatter_add, check=True)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -248,9 +279,11 @@ def _c5_worker(rank, world, n, d, b, seed):
 
     u_loc = torch.from_numpy(users[rank * b:(rank + 1) * b])
     grad_shard = torch.zeros((cnt, d))
+    status = torch.zeros(2, dtype=torch.int64)
     loss, du, dp = sharded_inbatch_step(shard, beg, u_loc, torch.from_numpy(ids[rank * b:(rank + 1) * b]), 0.1,
                                         gather=window_gather, loss_fn=cpu_loss, grad_shard=grad_shard,
-                                        scatter_add=scatter_add)
+                                        scatter_add=scatter_add, status=status)
+    assert status[0] == status[1] == world * b  # the owned count rode in the loss all-reduce
     dp_sum = dp.clone()
     torch.distributed.all_reduce(dp_sum)  # the frozen path exchanges nothing: sum here to compare
     # equals the single-process reference loss over the whole global batch

@@ -290,6 +290,32 @@ def test_flat_l2_index_vs_oracle(K, d, k, nx):
     assert ids[0][0] == "i0" and dist[0] == sorted(dist[0])
 
 
+@pytest.mark.parametrize("k,n_clus", [(10, 300), (100, 300)])
+def test_flat_l2_clustered_near_ties(K, k, n_clus):
+    """A cluster of near-duplicates around the queries: their distances differ
+    far below fp32 rounding of ||q||^2 + ||x||^2 - 2 q.x, so the augmented
+    selection score cannot rank them and k + 32 candidates miss Faiss's own
+    choice. The finish's certificate flags those queries, they are re-selected
+    with 512 candidates, and the result is bit-exact vs the oracle again."""
+    from rtrec_amd import kernels as KK
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex
+    rng = np.random.default_rng(77 + k)
+    d = 64
+    base = rng.standard_normal(d).astype(np.float32)
+    clus = (base + rng.standard_normal((n_clus, d)).astype(np.float32) * 1e-4).astype(np.float32)
+    far = (rng.standard_normal((2000, d)) * 3).astype(np.float32)
+    emb = np.concatenate([far[:1000], clus, far[1000:]])
+    q = (base + rng.standard_normal((16, d)).astype(np.float32) * 1e-4).astype(np.float32)
+    idx = HipFlatIPIndex({"dimension": d, "metric": "l2"})
+    idx.build(emb, [str(j) for j in range(len(emb))])
+    before = dict(KK.L2_STATS)
+    gs, gi = idx.search_tensors(q, k)
+    rs, ri = orc.flat_l2_search(q, emb, k, nthreads=8)
+    _l2_check(rs, ri, gs.cpu().numpy(), gi.cpu().numpy())
+    assert KK.L2_STATS["reselected"] > before["reselected"]   # the certificate fired
+    assert KK.L2_STATS["uncertified"] == before["uncertified"]
+
+
 def test_flat_l2_save_load_and_errors(K, tmp_path):
     from rtrec_amd.serving.retrieval import HipFlatIPIndex, read_flat_index
     rng = np.random.default_rng(9)
