@@ -96,7 +96,9 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
  * thread-safe, results unchanged by any setting). v4_mode: 0 automatic, 1 never
  * the sampled-threshold kernel pair, 2 it wherever legal (16-bit, d <= 128,
  * k <= 128); + 4: per-split thresholds instead of one corpus-wide threshold
- * per query when the items are split. v4_stride: sample every stride-th 128-row stage (0 = planner).
+ * per query when the items are split; + 8: fp32 corpora of <= 4096 rows keep
+ * the fused register-list scan instead of the score-slab GEMM + per-query
+ * select pair (the default for them). v4_stride: sample every stride-th 128-row stage (0 = planner).
  * v4_rank: threshold = rank-th largest sampled group maximum (-1 = planner,
  * 0 = no sample: a running threshold from -inf). Set before sizing the
  * workspace. */

@@ -41,6 +41,53 @@ struct BwdLaunch {
     bool vec0, vec1;              // dW: float4 staging loads
 };
 
+
+// ---------------------------------------------------------------------------
+// phase probe (diagnostic builds only: -DRT_PHASE_PROBE, tools/c2_phase_probe.py)
+// Thread 0 of every block stamps the shader clock at phase boundaries and
+// the 100 MHz real-time clock at entry and exit; at exit it appends one
+// 8-word record [tag<<32 | block, rt_start, m0, m1, m2, end, rt_end, xcc] to a
+// device buffer. Product builds compile none of this.
+#ifdef RT_PHASE_PROBE
+__device__ unsigned long long* g_probe_buf = nullptr;
+__device__ unsigned int g_probe_ctr[64];  // sharded by blockIdx % 64 (one counter: same-address atomics serialise)
+__device__ unsigned int g_probe_cap = 0;  // records per shard
+struct PhaseProbe {
+    uint64_t rt0 = 0, t0 = 0, m[4] = {0, 0, 0, 0};
+    __device__ __forceinline__ void start() {
+        if (threadIdx.x == 0) {
+            rt0 = __builtin_amdgcn_s_memrealtime();
+            t0 = __builtin_amdgcn_s_memtime();
+        }
+    }
+    __device__ __forceinline__ void mark(int i) {
+        if (threadIdx.x == 0) m[i] = __builtin_amdgcn_s_memtime() - t0;
+    }
+    __device__ __forceinline__ void end(unsigned tag) {
+        if (threadIdx.x == 0) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            m[3] = __builtin_amdgcn_s_memtime() - t0;
+            const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
+            const unsigned sh = blockIdx.x & 63u;
+            const unsigned slot = atomicAdd(&g_probe_ctr[sh], 1u);
+            if (slot < g_probe_cap && g_probe_buf) {
+                unsigned long long* o = g_probe_buf + (static_cast<uint64_t>(slot) * 64 + sh) * 8;
+                o[0] = (static_cast<uint64_t>(tag) << 32) | blockIdx.x;
+                o[1] = rt0; o[2] = m[0]; o[3] = m[1]; o[4] = m[2]; o[5] = m[3]; o[6] = rt1; o[7] = xcc;
+            }
+        }
+    }
+};
+#define RT_PP_DECL PhaseProbe pp_; pp_.start();
+#define RT_PP_MARK(i) pp_.mark(i);
+#define RT_PP_END(tag) pp_.end(tag);
+#else
+#define RT_PP_DECL
+#define RT_PP_MARK(i)
+#define RT_PP_END(tag)
+#endif
+
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -103,7 +150,7 @@ constexpr int FM = 32;  // rows per block
 __host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // kh % 16 == 0
 
 template <int TPW, bool KVEC>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
-__global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 2))) void linear_fwd_kernel(FwdLaunch L) {
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_fwd_args& a = g1 ? L.a1 : L.a0;
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
@@ -120,6 +167,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
     const int64_t row0 = static_cast<int64_t>(bid) * FM;
     const int64_t m = a.m;
+    RT_PP_DECL
     if (blockIdx.x == 0 && a.zero_buf)
         for (int64_t e = tid; e < a.zero_words; e += 256) a.zero_buf[e] = 0.0;
 
@@ -131,6 +179,43 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
     const bool fast = vec && (a.k % 4) == 0 && (256 % vpr) == 0 &&
                       (a.prev_mode == 0 || act_is_piecewise_linear(a.prev_act));
     const bool early = fast && !a.ids && 8 * (256 / vpr) >= FM;  // one pass covers the tile
+    // one-tile waves (every C2 layer but the first) request their first W
+    // fragments before the prologue (they do not depend on it), so the L2
+    // latency hides behind the A-tile staging (wider waves would spill)
+    const float* wrow[TPW];
+    bool tile_on[TPW], row_ok[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        tile_on[i] = (w + 4 * i) * 32 < n;  // wave-uniform
+        const int nn = (w + 4 * i) * 32 + c32;
+        row_ok[i] = nn < n;
+        wrow[i] = a.w + static_cast<int64_t>(row_ok[i] ? nn : 0) * k;
+    }
+    // 16 k-steps per iteration (kh % 16 == 0); the W fragments of the next
+    // iteration are loaded during this one's MFMAs (register double buffer)
+    float4 wv[TPW][4], wn[TPW][4];
+    auto load_w = [&](int s, float4 (&dst)[TPW][4]) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kk = h * kh + s + 4 * j;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (tile_on[i] && row_ok[i]) {
+                    const float* wr = wrow[i] + kk;
+                    if constexpr (KVEC) {
+                        if (kk < k) v = *reinterpret_cast<const float4*>(wr);
+                    } else {
+                        if (kk < k) v.x = wr[0];
+                        if (kk + 1 < k) v.y = wr[1];
+                        if (kk + 2 < k) v.z = wr[2];
+                        if (kk + 3 < k) v.w = wr[3];
+                    }
+                }
+                dst[i][j] = v;
+            }
+    };
+    if constexpr (TPW == 1) load_w(0, wn);
     float4 pre[8];
     if (early) {
         const int c = (tid % vpr) * 4, rstep = 256 / vpr, r0 = tid / vpr;
@@ -194,6 +279,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
         srow[tid] = sr;
     }
     __syncthreads();
+    RT_PP_MARK(0)
     const uint64_t seed = a.drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.drop_p, a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f, seed,
                   scale, shift};
@@ -282,45 +368,13 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
         }
     }
     __syncthreads();
+    RT_PP_MARK(1)
 
     f32x16 acc[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) acc[i] = f32x16{};
     const float* ap = As + c32 * lda + h * kh;
-    const float* wrow[TPW];
-    bool tile_on[TPW], row_ok[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-        tile_on[i] = (w + 4 * i) * 32 < n;  // wave-uniform
-        const int nn = (w + 4 * i) * 32 + c32;
-        row_ok[i] = nn < n;
-        wrow[i] = a.w + static_cast<int64_t>(row_ok[i] ? nn : 0) * k;
-    }
-    // 16 k-steps per iteration (kh % 16 == 0); the W fragments of the next
-    // iteration are loaded during this one's MFMAs (register double buffer)
-    float4 wv[TPW][4], wn[TPW][4];
-    auto load_w = [&](int s, float4 (&dst)[TPW][4]) {
-#pragma unroll
-        for (int i = 0; i < TPW; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int kk = h * kh + s + 4 * j;
-                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (tile_on[i] && row_ok[i]) {
-                    const float* wr = wrow[i] + kk;
-                    if constexpr (KVEC) {
-                        if (kk < k) v = *reinterpret_cast<const float4*>(wr);
-                    } else {
-                        if (kk < k) v.x = wr[0];
-                        if (kk + 1 < k) v.y = wr[1];
-                        if (kk + 2 < k) v.z = wr[2];
-                        if (kk + 3 < k) v.w = wr[3];
-                    }
-                }
-                dst[i][j] = v;
-            }
-    };
-    load_w(0, wn);
+    if constexpr (TPW != 1) load_w(0, wn);
     for (int s = 0; s < kh; s += 16) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
@@ -343,6 +397,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
         }
     }
 
+    RT_PP_MARK(2)
     // ---- epilogue ----
     const bool l2 = a.l2_out != nullptr;
     // final layer, fast form: z² staged column-major in the (now idle) A tile,
@@ -392,6 +447,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
                 if (gr < m && col < n) a.l2_out[gr * n + col] = acc[i][r] * rowpart[lr];
             }
         }
+        RT_PP_END(1)
         return;
     }
     double* const stats = a.stats_out ? a.stats_out + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
@@ -468,6 +524,7 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(FwdLaunch L) {
             }
         }
     }
+    RT_PP_END(1)
 }
 
 // ---------------------------------------------------------------------------
@@ -492,6 +549,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     const bool two = a.seg_split > 0;
     const int my_seg = (two && row0 >= a.seg_split) ? 1 : 0;
     const int64_t seg_m = two ? (my_seg == 0 ? a.seg_split : m - a.seg_split) : m;
+    RT_PP_DECL
 
     // ---- phase A: dz tile ----
     const int l4 = n / 4;  // grad_mode 0 fast path: float4 lanes per row (a power of two <= 64)
@@ -699,6 +757,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             }
         }
     }
+    RT_PP_MARK(0)
     if (a.dbias && a.dbias_slots) {
         // dbias partials: this block's column sums of dz into fp64 slot bid % SLOTS
         // (the dW launch folds the slots; contention per address = blocks / SLOTS)
@@ -723,8 +782,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             }
         }
     }
-    if (!a.g_prev && !a.dsrc) return;
+    if (!a.g_prev && !a.dsrc) {
+        RT_PP_END(2)
+        return;
+    }
     __syncthreads();
+    RT_PP_MARK(1)
 
     // ---- phase B: dA = dz · W  (reduction over n, permuted per lane half) ----
     f32x16 acc[TPWK];
@@ -788,6 +851,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             acc[i] = mfma(av[1].w, wv[i][7], acc[i]);
         }
     }
+    RT_PP_MARK(2)
     const float pscale = a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f;
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     double* const gps = want_stats ? a.g_prev_stats + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
@@ -846,6 +910,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             }
         }
     }
+    RT_PP_END(2)
 }
 
 // ---------------------------------------------------------------------------
@@ -902,6 +967,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     __shared__ __attribute__((aligned(16))) float Ld[2][DW_R * LDN];
     __shared__ __attribute__((aligned(16))) float La[2][DW_R * LDK];
     __shared__ int srow[DW_MAXR];
+    __shared__ __attribute__((aligned(16))) float aff_s[2][2][BK];  // [segment][scale, shift][tile column]
 
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args a = g1 ? L.a1 : L.a0;  // by value: fields loaded once
@@ -917,6 +983,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     const int64_t r_begin = static_cast<int64_t>(bz) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
     if (r_begin >= m) return;  // a padding split (block-uniform, before any barrier)
+    RT_PP_DECL
     const bool gather = a.ids != nullptr;
     const bool two = a.seg_split > 0;
 
@@ -927,13 +994,23 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     float4 sc0 = make_float4(1.f, 1.f, 1.f, 1.f), sc1 = sc0;
     float4 sh0 = make_float4(0.f, 0.f, 0.f, 0.f), sh1 = sh0;
     if (a.prev_mode == 1 || a.prev_mode == 2) {
-        auto aff = [&](int sg, int i, float& scv, float& shv) {
-            const int cc = gk + i;
+        // one load per (segment, column) for the whole block, through LDS: with
+        // every thread loading its own 4 columns x 2 segments x 4 arrays, the
+        // 512 threads x ~750 blocks of a C2 launch hammered the same few L2
+        // lines (7.4 us of prologue per block, tools/c2_phase_probe.py)
+        if (tid < 2 * BK) {
+            const int sg = tid / BK, cl = tid % BK, cc = k0 + cl;
             const int so = two ? sg * k : 0;
+            float scv = 1.f, shv = 0.f;
             if (cc < k) bn_affine(a.prev_gamma[cc], a.prev_beta[cc], a.prev_mean[so + cc], a.prev_invstd[so + cc], scv, shv);
-        };
-        aff(0, 0, sc0.x, sh0.x); aff(0, 1, sc0.y, sh0.y); aff(0, 2, sc0.z, sh0.z); aff(0, 3, sc0.w, sh0.w);
-        aff(1, 0, sc1.x, sh1.x); aff(1, 1, sc1.y, sh1.y); aff(1, 2, sc1.z, sh1.z); aff(1, 3, sc1.w, sh1.w);
+            aff_s[sg][0][cl] = scv;
+            aff_s[sg][1][cl] = shv;
+        }
+        __syncthreads();
+        sc0 = *reinterpret_cast<const float4*>(&aff_s[0][0][ck]);
+        sh0 = *reinterpret_cast<const float4*>(&aff_s[0][1][ck]);
+        sc1 = *reinterpret_cast<const float4*>(&aff_s[1][0][ck]);
+        sh1 = *reinterpret_cast<const float4*>(&aff_s[1][1][ck]);
     }
     const uint64_t pseed = a.prev_drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
@@ -1035,9 +1112,11 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     const int ncol = (w % NTN) * 32 + c;       // this lane's dz column inside the tile
     const int kcol0 = (w / NTN) * T * 32 + c;  // this lane's first A column inside the tile
     int buf = 0;
+    RT_PP_MARK(0)
     load(r_begin);
     store(0, r_begin);
     __syncthreads();
+    RT_PP_MARK(1)
     for (int64_t base = r_begin; base < r_end; base += DW_R) {
         const bool more = base + DW_R < r_end;  // block-uniform
         if (more) load(base + DW_R);            // in flight during the MFMAs below
@@ -1063,6 +1142,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     // hands the other half of its accumulators to the other group through the
     // (idle) dz buffers (both groups issue atomics: 1.5 µs/step faster than
     // group 0 adding all of it); the dbias partials go through the A buffers.
+    RT_PP_MARK(2)
     float* red = &Ld[0][0];
     float* bred = &La[0][0];  // [8 waves][VN][4]
     if (do_bias) {
@@ -1109,6 +1189,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         for (int r = 0; r < 16; ++r)
             if ((r >> 3) == grp) add_row(t, r, kk);
     }
+    RT_PP_END(3)
 }
 
 }  // namespace mlp
@@ -1335,6 +1416,22 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
 extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream) {
     return rt_linear_bwd_dw_f32_multi(args, 1, stream);
 }
+
+#ifdef RT_PHASE_PROBE
+// diagnostic builds only (not part of the ABI header)
+extern "C" int rt_probe_setup(void* buf, unsigned cap) {
+    unsigned long long* p = static_cast<unsigned long long*>(buf);
+    const unsigned zero[64] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mlp::g_probe_buf), &p, sizeof(p)) != hipSuccess) return RT_ERR_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mlp::g_probe_cap), &cap, sizeof(cap)) != hipSuccess) return RT_ERR_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(mlp::g_probe_ctr), zero, sizeof(zero)) != hipSuccess) return RT_ERR_HIP;
+    return RT_OK;
+}
+extern "C" int rt_probe_count(unsigned* out) {  // 64 shard counters
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mlp::g_probe_ctr), 64 * sizeof(unsigned)) == hipSuccess ? RT_OK
+                                                                                                       : RT_ERR_HIP;
+}
+#endif
 
 extern "C" int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream) {
     const int rc = rt_linear_bwd_dz_f32(args, stream);

@@ -123,6 +123,7 @@ static int g_v4_mode = 0;     // 0 auto, 1 never, 2 wherever legal
 static int g_v4_stride = 0;   // 0: planner's choice
 static int g_v4_rank = -1;    // -1: planner's choice; 0: no sample (v2-style running threshold)
 static int g_v4_joint = 1;    // 1: over several splits, one corpus-wide threshold per query
+static int g_dense = 1;       // 1: fp32 small corpora take the GEMM + select pair (topk_dense.h)
 
 // log P(Bin(n, f) >= r)
 inline double log_binom_tail(int n, double f, int r) {
@@ -216,6 +217,16 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
 inline Plan make_plan(int64_t nq, int64_t nx, int d, int dtype, int k, const Shape& sh) {
     Plan p{};
     if (nx > 0 && plan_v4(nq, nx, d, dtype, k, p)) return p;
+    if (dtype == RT_F32 && g_dense && dense::applies(nx, d, k)) {
+        // the score slab of one query chunk (<= 256 MB: it stays in the Infinity Cache)
+        p.dense = 1;
+        p.chunk = dense::chunk_for(nq, nx);
+        p.q_tiles = 1;
+        p.splits = 1;
+        p.items_per_split = nx;
+        p.cand_bytes = static_cast<size_t>(p.chunk) * dense::ld_for(nx) * sizeof(float);
+        return p;
+    }
     p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
     if (p.chunk < 1) p.chunk = 1;
     p.q_tiles = static_cast<int>((p.chunk + sh.qt - 1) / sh.qt);
@@ -340,9 +351,11 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
 }
 
 extern "C" int rt_flatip_topk_tuning(int v4_mode, int v4_stride, int v4_rank) {
-    if (v4_mode < 0 || (v4_mode & 3) > 2 || v4_mode > 6 || v4_stride < 0 || v4_rank < -1 ||
+    if (v4_mode < 0 || (v4_mode & 3) > 2 || v4_mode > 14 || v4_stride < 0 || v4_rank < -1 ||
         v4_rank > 2 * topk::v4::kList)
         return RT_ERR_INVALID;
+    topk::g_dense = (v4_mode & 8) ? 0 : 1;
+    v4_mode &= 7;
     topk::g_v4_joint = (v4_mode & 4) ? 0 : 1;
     v4_mode &= 3;
     topk::g_v4_mode = v4_mode;

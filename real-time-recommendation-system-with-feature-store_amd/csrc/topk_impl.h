@@ -104,6 +104,7 @@ struct Plan {
     int stride, rank;    // v4 sample: every stride-th stage; threshold = rank-th group maximum
     size_t meta_bytes;   // v4 per-(split, query, half) entry counts
     size_t kth_bytes;    // register-list kernel over > 1 split: the shared per-query k-th keys
+    int dense;           // 1: fp32 small corpus, GEMM into a score slab + per-query select (topk_dense.h)
 };
 
 struct Args {
@@ -439,6 +440,7 @@ int launch_cfg(const Args& a, const Plan& p, hipStream_t st) {
 #include "topk_v2.h"
 #include "topk_v3.h"
 #include "topk_v4.h"
+#include "topk_dense.h"
 
 namespace rt {
 namespace topk {
@@ -470,6 +472,7 @@ int launch_S(const Args& a, const Plan& p, hipStream_t st) {
                                                p.v4_joint ? a.fail : nullptr, st);
     }
     if constexpr (F32) {
+        if (p.dense) return dense::launch(a, reinterpret_cast<float*>(a.cand), dense::ld_for(a.nx), st);
         switch (list_k(true, a.k)) {
             case 16: return launch_cfg<T, S, 16>(a, p, st);
             case 32: return launch_cfg<T, S, 32>(a, p, st);

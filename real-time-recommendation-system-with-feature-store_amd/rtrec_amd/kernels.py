@@ -129,7 +129,8 @@ def topk_tuning(v4_mode: int = 0, v4_stride: int = 0, v4_rank: int = -1) -> None
     """Planner override of flatip_topk (rt_flatip_topk_tuning; process-wide,
     results unchanged): v4_mode 0 automatic / 1 never / 2 wherever legal the
     sampled-threshold kernel pair (+4: per-split thresholds instead of one
-    corpus-wide threshold per query); v4_stride the sample stride in 128-row stages
+    corpus-wide threshold per query; +8: small fp32 corpora keep the fused
+    register-list scan instead of the score-slab GEMM + select); v4_stride the sample stride in 128-row stages
     (0 = planner); v4_rank the sampled rank (-1 = planner, 0 = no sample)."""
     call("rt_flatip_topk_tuning", int(v4_mode), int(v4_stride), int(v4_rank))
 
