@@ -169,7 +169,9 @@ int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* pos_items, in
  * b % RT_STAT_SLOTS (bounds same-address atomic contention), consumers sum the
  * slots in slot order. Caller zeroes them before the producing launch.
  * ------------------------------------------------------------------------ */
+#ifndef RT_STAT_SLOTS
 #define RT_STAT_SLOTS 16
+#endif
 
 typedef struct {
     const float* src;        /* [src_rows, ld_src] input rows (features or prev z) */
@@ -212,6 +214,9 @@ typedef struct {
                                 other work (a step's first launch clears the next
                                 accumulators: loss triple, per-tensor grad norms) */
     int64_t zero_words;
+    float* wt_out;           /* optional [k, n]: the launch also writes Wᵀ (row kk = column kk
+                                of w), which the backward's dz launch reads as rt_linear_bwd_args.wt
+                                (NULL = skip) */
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
@@ -267,6 +272,8 @@ typedef struct {
                                 adds each row block's column sums of dz (slot = block % SLOTS)
                                 and the dW launch folds the slots into dbias — bounded
                                 same-address contention; NULL = the dW launch sums dz itself */
+    const float* wt;         /* optional [k, n] = Wᵀ of THIS step's w (rt_linear_fwd_args.wt_out):
+                                dA = dz·W then reads contiguous rows of it (NULL = columns of w) */
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);

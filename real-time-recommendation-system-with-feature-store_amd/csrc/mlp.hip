@@ -88,6 +88,33 @@ struct PhaseProbe {
 #define RT_PP_END(tag)
 #endif
 
+// Stores of the big per-row activations (z, dz, the next layer's g) are
+// write-through (sc1): the lines leave L2 during the kernel instead of in the
+// write-back at the kernel boundary (≈ dirty bytes / 6 TB/s per boundary;
+// z1 alone is 18.9 MB), at the price of the next kernel reading them from the
+// Infinity Cache instead of L2. Same-box A/B of the C2 step, 3 rounds x 200
+// steps: 0.2835-0.2840 vs 0.2895-0.2903 ms (profiles/r04_c2_ab_stores.txt).
+// -DRT_NO_WT_STORES builds the plain-store form.
+#if !defined(RT_NO_WT_STORES)
+#define RT_WT_STORES 1
+#endif
+__device__ __forceinline__ void st_act(float* p, float v) {
+#ifdef RT_WT_STORES
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void st_act4(float* p, float4 v) {
+#ifdef RT_WT_STORES
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+#else
+    *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -179,6 +206,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     const bool fast = vec && (a.k % 4) == 0 && (256 % vpr) == 0 &&
                       (a.prev_mode == 0 || act_is_piecewise_linear(a.prev_act));
     const bool early = fast && !a.ids && 8 * (256 / vpr) >= FM;  // one pass covers the tile
+    // Wᵀ for the backward's dz launch (rt_linear_fwd_args.wt_out): blocks
+    // 0 .. tiles-1 of each group each copy one 32x32 tile of W, transposed
+    // (float4 reads along k, scattered 4-byte writes; 32 tiles at the C2 layer 2)
+    if (a.wt_out) {
+        const int tk = (k + 31) / 32, tiles = tk * ((n + 31) / 32);
+        if (static_cast<int>(bid) < tiles) {
+            const int n0 = (static_cast<int>(bid) / tk) * 32, k0 = (static_cast<int>(bid) % tk) * 32;
+            const int r = tid >> 3, c = (tid & 7) * 4;
+            if (n0 + r < n) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (k0 + c + j < k) a.wt_out[static_cast<int64_t>(k0 + c + j) * n + n0 + r] = a.w[static_cast<int64_t>(n0 + r) * k + k0 + c + j];
+            }
+        }
+    }
     // one-tile waves (every C2 layer but the first) request their first W
     // fragments before the prologue (they do not depend on it), so the L2
     // latency hides behind the A-tile staging (wider waves would spill)
@@ -444,7 +486,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
             for (int r = 0; r < 16; ++r) {
                 const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
                 const int64_t gr = row0 + lr;
-                if (gr < m && col < n) a.l2_out[gr * n + col] = acc[i][r] * rowpart[lr];
+                if (gr < m && col < n) st_act(a.l2_out + gr * n + col, acc[i][r] * rowpart[lr]);
             }
         }
         RT_PP_END(1)
@@ -468,7 +510,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const float z = acc[i][r] + b;
-                if (col_ok) zp[((r & 3) + 8 * (r >> 2)) * n] = z;
+                if (col_ok) st_act(zp + ((r & 3) + 8 * (r >> 2)) * n, z);
                 const float av = act_pwl(sl, z);
                 s1 += av;
                 s2 += av * av;
@@ -482,7 +524,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
             const float z = acc[i][r] + b;
             acc[i][r] = z;
             const bool ok = col_ok && gr < m;
-            if (ok && a.z_out) a.z_out[gr * n + col] = z;
+            if (ok && a.z_out) st_act(a.z_out + gr * n + col, z);
             if (ok && stats) {
                 const float av = act_eval(a.act, z);
                 s1 += av;
@@ -587,7 +629,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                 d.y = big ? (dv[p].y - lv[p].y * dot) * inv : dv[p].y * inv;
                 d.z = big ? (dv[p].z - lv[p].z * dot) * inv : dv[p].z * inv;
                 d.w = big ? (dv[p].w - lv[p].w * dot) * inv : dv[p].w * inv;
-                *reinterpret_cast<float4*>(a.dz_ws + gr * n + c) = d;
+                st_act4(a.dz_ws + gr * n + c, d);
             }
             *reinterpret_cast<float4*>(Dz + r * ldz + c) = d;
         }
@@ -699,7 +741,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                     d.w = one(gv[u].w, zv[u].w, fA.w, fB.w, fC.w, fM.w, fI.w);
                     if (gr >= m || c >= n) d = make_float4(0.f, 0.f, 0.f, 0.f);
                     *reinterpret_cast<float4*>(Dz + r * ldz + c) = d;
-                    if (gr < m && c < n) *reinterpret_cast<float4*>(a.dz_ws + gr * n + c) = d;
+                    if (gr < m && c < n) st_act4(a.dz_ws + gr * n + c, d);
                 }
             }
         } else
@@ -816,15 +858,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
 #pragma unroll
         for (int r = 0; r < 16; ++r) zpre[i][r] = ld ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
     }
+    // with Wᵀ (a.wt, n % 8 == 0) a lane's 8 consecutive n of column kk are one
+    // contiguous 32-byte run: two float4 loads instead of eight strided ones
+#ifdef RT_NO_WT_ROWS  // A/B variant: the strided column loads of w
+    const float* __restrict__ WtT = nullptr;
+#else
+    const float* __restrict__ WtT = (a.wt && (n % 8) == 0) ? a.wt : nullptr;
+#endif
     auto load_w = [&](int s, float (&dst)[TPWK][8]) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
             const int kk = (w + 4 * i) * 32 + c32;
             const bool on = (w + 4 * i) * 32 < k && kk < k;
+            if (WtT) {
+                const int nn = h * nh + s;
+                float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+                if (on && nn < n) {
+                    const float* p = WtT + static_cast<int64_t>(kk) * n + nn;
+                    v0 = *reinterpret_cast<const float4*>(p);
+                    v1 = *reinterpret_cast<const float4*>(p + 4);
+                }
+                dst[i][0] = v0.x; dst[i][1] = v0.y; dst[i][2] = v0.z; dst[i][3] = v0.w;
+                dst[i][4] = v1.x; dst[i][5] = v1.y; dst[i][6] = v1.z; dst[i][7] = v1.w;
+            } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int nn = h * nh + s + j;
-                dst[i][j] = (on && nn < n) ? Wt[static_cast<int64_t>(nn) * k + kk] : 0.f;
+                for (int j = 0; j < 8; ++j) {
+                    const int nn = h * nh + s + j;
+                    dst[i][j] = (on && nn < n) ? Wt[static_cast<int64_t>(nn) * k + kk] : 0.f;
+                }
             }
         }
     };
@@ -874,7 +935,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                 const int lr = (r & 3) + 8 * (r >> 2);
                 float gv = acc[i][r];
                 if (drop) gv = dropout_keep(pseed, rb + lr, kk, a.prev_drop_p) ? gv * pscale : 0.f;
-                if (col_ok) gp[lr * k] = gv;
+                if (col_ok) st_act(gp + lr * k, gv);
                 const float xh = (act_pwl(psl, zv[r]) - pm) * pi;
                 s1 += gv;
                 s2 += gv * xh;

@@ -201,6 +201,7 @@ class ChainCtx:
     norms: Optional[torch.Tensor] = None
     normalize: bool = True
     seg_split: int = 0  # > 0: rows [0, seg_split) and [seg_split, m) are separate BN batches
+    wts: List[Optional[torch.Tensor]] = field(default_factory=list)  # Wᵀ of each Linear (fwd writes, dz reads)
 
 
 def _stream(t: torch.Tensor):
@@ -344,6 +345,12 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
                 if pb.bn.training and pb.bn.num_batches_tracked is not None:
                     a.num_batches_tracked = pb.bn.num_batches_tracked.data_ptr()  # +1 in-kernel
         a.act = b.act
+        # Wᵀ of this Linear for its backward's dA (layers past the first: their
+        # dz launch computes the previous block's gradient)
+        wt = torch.empty((lin.in_features, lin.out_features), dtype=torch.float32, device=dev) if li > 0 else None
+        if wt is not None:
+            a.wt_out = wt.data_ptr()
+        ctx.wts.append(wt)
         if li < L:
             z = torch.empty((m, lin.out_features), dtype=torch.float32, device=dev)
             a.z_out = z.data_ptr()
@@ -506,5 +513,7 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
             gs[li - 1] = g
             keep.append(g)
             a.g_prev = g.data_ptr()
+            if li < len(ctx.wts) and ctx.wts[li] is not None:
+                a.wt = ctx.wts[li].data_ptr()
         layers.append(a)
     return layers, dsrc, keep

@@ -15,11 +15,13 @@ else
   git -C $R archive $REV $PKG/csrc include | tar -x -C $T
   mv $T/$PKG/csrc/* $T/csrc/
 fi
+pids=()
 for f in $T/csrc/*.hip; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -Wno-unused-function \
     -I$T/include -I$T/csrc "$@" -c $f -o $T/obj/$(basename $f .hip).o &
+  pids+=($!)
 done
-wait
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT $T/obj/*.o
+for p in "${pids[@]}"; do wait $p || { echo "compile failed"; exit 1; }; done
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT.tmp $T/obj/*.o && mv -f $OUT.tmp $OUT
 rm -rf $T
 echo built $OUT
