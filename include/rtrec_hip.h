@@ -170,7 +170,7 @@ int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* pos_items, in
  * slots in slot order. Caller zeroes them before the producing launch.
  * ------------------------------------------------------------------------ */
 #ifndef RT_STAT_SLOTS
-#define RT_STAT_SLOTS 16
+#define RT_STAT_SLOTS 8
 #endif
 
 typedef struct {

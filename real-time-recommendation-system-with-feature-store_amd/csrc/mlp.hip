@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
             }
         }
     }
+    RT_PP_MARK(0)  // thread 0's BN finalisation done (its early A loads may still be in flight)
     if (tid < FM) {
         const int64_t gr = row0 + tid;
         int64_t sr = -1;
@@ -321,7 +322,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
         srow[tid] = sr;
     }
     __syncthreads();
-    RT_PP_MARK(0)
     const uint64_t seed = a.drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
     const Pro pro{a.prev_mode, a.prev_act, a.drop_p, a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f, seed,
                   scale, shift};
@@ -593,6 +593,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     const int64_t seg_m = two ? (my_seg == 0 ? a.seg_split : m - a.seg_split) : m;
     RT_PP_DECL
 
+    // one-tile waves request dA's first W fragments here, ahead of phase A
+    // (they do not depend on it), so their latency hides behind the dz tile
+    // 8 k-steps per iteration (nh % 16 == 0); next iteration's W loaded during this one's MFMAs
+    float wv[TPWK][8], wn[TPWK][8];
+    // (the W pointer read once: inside the conditional loads below a field of
+    // the selected launch group was re-loaded from the kernarg segment per load)
+    const float* __restrict__ Wt = a.w;
+    // with Wᵀ (a.wt, n % 8 == 0) a lane's 8 consecutive n of column kk are one
+    // contiguous 32-byte run: two float4 loads instead of eight strided ones
+#ifdef RT_NO_WT_ROWS  // A/B variant: the strided column loads of w
+    const float* __restrict__ WtT = nullptr;
+#else
+    const float* __restrict__ WtT = (a.wt && (n % 8) == 0) ? a.wt : nullptr;
+#endif
+    auto load_w = [&](int s, float (&dst)[TPWK][8]) {
+#pragma unroll
+        for (int i = 0; i < TPWK; ++i) {
+            const int kk = (w + 4 * i) * 32 + c32;
+            const bool on = (w + 4 * i) * 32 < k && kk < k;
+            if (WtT) {
+                const int nn = h * nh + s;
+                float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+                if (on && nn < n) {
+                    const float* p = WtT + static_cast<int64_t>(kk) * n + nn;
+                    v0 = *reinterpret_cast<const float4*>(p);
+                    v1 = *reinterpret_cast<const float4*>(p + 4);
+                }
+                dst[i][0] = v0.x; dst[i][1] = v0.y; dst[i][2] = v0.z; dst[i][3] = v0.w;
+                dst[i][4] = v1.x; dst[i][5] = v1.y; dst[i][6] = v1.z; dst[i][7] = v1.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int nn = h * nh + s + j;
+                    dst[i][j] = (on && nn < n) ? Wt[static_cast<int64_t>(nn) * k + kk] : 0.f;
+                }
+            }
+        }
+    };
+    if constexpr (TPWK == 1) {  // (two-tile waves would spill)
+        if (a.g_prev || a.dsrc) load_w(0, wn);
+    }
+
     // ---- phase A: dz tile ----
     const int l4 = n / 4;  // grad_mode 0 fast path: float4 lanes per row (a power of two <= 64)
     if (a.grad_mode == 0 && (n % 4) == 0 && l4 <= 64 && (l4 & (l4 - 1)) == 0 && np == n) {
@@ -836,11 +878,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) acc[i] = f32x16{};
     const float* dp = Dz + c32 * ldz + h * nh;
-    // 8 k-steps per iteration (nh % 16 == 0); next iteration's W loaded during this one's MFMAs
-    float wv[TPWK][8], wn[TPWK][8];
-    // (the W pointer read once: inside the conditional loads below a field of
-    // the selected launch group was re-loaded from the kernarg segment per load)
-    const float* __restrict__ Wt = a.w;
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
     // fast epilogue (the C2 hidden layers): a full row block, g_prev only, a
     // piecewise-linear previous activation — no per-element predicates, 32-bit
@@ -858,38 +895,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
 #pragma unroll
         for (int r = 0; r < 16; ++r) zpre[i][r] = ld ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
     }
-    // with Wᵀ (a.wt, n % 8 == 0) a lane's 8 consecutive n of column kk are one
-    // contiguous 32-byte run: two float4 loads instead of eight strided ones
-#ifdef RT_NO_WT_ROWS  // A/B variant: the strided column loads of w
-    const float* __restrict__ WtT = nullptr;
-#else
-    const float* __restrict__ WtT = (a.wt && (n % 8) == 0) ? a.wt : nullptr;
-#endif
-    auto load_w = [&](int s, float (&dst)[TPWK][8]) {
-#pragma unroll
-        for (int i = 0; i < TPWK; ++i) {
-            const int kk = (w + 4 * i) * 32 + c32;
-            const bool on = (w + 4 * i) * 32 < k && kk < k;
-            if (WtT) {
-                const int nn = h * nh + s;
-                float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-                if (on && nn < n) {
-                    const float* p = WtT + static_cast<int64_t>(kk) * n + nn;
-                    v0 = *reinterpret_cast<const float4*>(p);
-                    v1 = *reinterpret_cast<const float4*>(p + 4);
-                }
-                dst[i][0] = v0.x; dst[i][1] = v0.y; dst[i][2] = v0.z; dst[i][3] = v0.w;
-                dst[i][4] = v1.x; dst[i][5] = v1.y; dst[i][6] = v1.z; dst[i][7] = v1.w;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int nn = h * nh + s + j;
-                    dst[i][j] = (on && nn < n) ? Wt[static_cast<int64_t>(nn) * k + kk] : 0.f;
-                }
-            }
-        }
-    };
-    load_w(0, wn);
+    if constexpr (TPWK != 1) load_w(0, wn);
     for (int s = 0; s < nh; s += 8) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i)

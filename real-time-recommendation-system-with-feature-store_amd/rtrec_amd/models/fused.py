@@ -208,7 +208,10 @@ def _stream(t: torch.Tensor):
     return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
 
-STAT_SLOTS = 16  # RT_STAT_SLOTS (include/rtrec_hip.h): BN sums are [slots][2][width] fp64
+# BN sums are [slots][2][width] fp64 (include/rtrec_hip.h RT_STAT_SLOTS, 8 in
+# this build); the arenas are sized for 16, an upper bound of every library
+# variant's slot count, so a variant build never writes past them
+STAT_SLOTS = 16
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
