@@ -274,9 +274,18 @@ typedef struct {
                                 same-address contention; NULL = the dW launch sums dz itself */
     const float* wt;         /* optional [k, n] = Wᵀ of THIS step's w (rt_linear_fwd_args.wt_out):
                                 dA = dz·W then reads contiguous rows of it (NULL = columns of w) */
+    int fuse_dz;             /* 1: a layer with no dA (g_prev and dsrc NULL), grad_mode 1-3, a
+                                piecewise-linear act and n % 4 == 0 (16-B aligned g, z) computes
+                                dz inside its dW launch: the dz launch of the pair is then a no-op
+                                and dz_ws is NOT written; dbias, dgamma, dbeta come from the dW
+                                launch (ignored when the layer does not qualify) */
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);
+/* 1 when the dz launch of these (1 or 2) argument sets is a no-op because
+ * their dW launch computes dz itself (rt_linear_bwd_args.fuse_dz), else 0 —
+ * the caller may then skip the dz call. Host-only, no GPU work. */
+int rt_linear_bwd_dz_fused(const rt_linear_bwd_args* args, int n_args);
 /* the two launches of rt_linear_bwd_f32, separately (same arguments, same
  * order on one stream): dz/dgamma/dbeta/dA, then dW/dbias from dz_ws. */
 int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream);

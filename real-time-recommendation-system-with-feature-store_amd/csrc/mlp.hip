@@ -1021,7 +1021,12 @@ __device__ __forceinline__ float pro_col(const Pro& p, float slope, int64_t r, i
     }
 }
 
-template <int BN, int BK, int PRO, bool VEC>  // VEC: n, k, ld_src multiples of 4, 16-B aligned rows
+// DZF: the layer has no dA (the first Linear of a chain); the dz launch was
+// skipped (rt_linear_bwd_args.fuse_dz) and dz is computed here while staged,
+// from g and z with the per-column BN-backward coefficients, exactly as the dz
+// launch's phase A would; dgamma/dbeta (block 0) and dbias (row sums of the
+// computed dz) are added here too.
+template <int BN, int BK, int PRO, bool VEC, bool DZF>  // VEC: n, k, ld_src multiples of 4, 16-B aligned rows
 __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     constexpr int NTN = BN / 32, WK = 4 / NTN, T = (BK / 32) / WK;
     static_assert(NTN * 32 == BN && 4 % NTN == 0 && T >= 1 && T * WK * 32 == BK, "dW tile");
@@ -1035,6 +1040,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     __shared__ __attribute__((aligned(16))) float La[2][DW_R * LDK];
     __shared__ int srow[DW_MAXR];
     __shared__ __attribute__((aligned(16))) float aff_s[2][2][BK];  // [segment][scale, shift][tile column]
+    __shared__ __attribute__((aligned(16))) float dzc_s[DZF ? 2 : 1][5][DZF ? BN : 4];  // DZF: [seg][A,B,C,M,I][col]
 
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args a = g1 ? L.a1 : L.a0;  // by value: fields loaded once
@@ -1083,9 +1089,46 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     const Pro pro{a.prev_mode, a.prev_act, a.prev_drop_p, a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f,
                   pseed, nullptr, nullptr};
     const float slope = act_slope(a.prev_act);
-    // dbias: folded from the dz launch's fp64 slots by block 0, or (no slots)
-    // summed here by the k-tile-0 blocks
-    if (a.dbias && a.dbias_slots && bid == 0) {
+    if constexpr (DZF) {
+        // per-column BN-backward coefficients of this block's n-tile, per row
+        // segment (the dz launch's phase A): A = γ·invstd (or 1), B = Σg/m,
+        // C = Σg·x̂/m, M = mean, I = invstd
+        if (tid < 2 * BN) {
+            const int sg = tid / BN, cl = tid % BN, c = n0 + cl;
+            const int my = two ? sg : 0;
+            const int64_t seg_m = two ? (my == 0 ? a.seg_split : m - a.seg_split) : m;
+            float A = 1.f, Bc = 0.f, C = 0.f, M = 0.f, I = 1.f;
+            if (c < n && (a.grad_mode == 1 || a.grad_mode == 2)) {
+                I = a.save_invstd[my * n + c];
+                M = a.save_mean[my * n + c];
+                A = a.bn_gamma[c] * I;
+                if (a.grad_mode == 1) {
+                    double gs1, gs2;
+                    slot_sums(a.g_stats + static_cast<int64_t>(my) * RT_STAT_SLOTS * 2 * n, n, c, gs1, gs2);
+                    const float inv_m = 1.f / static_cast<float>(seg_m);
+                    Bc = static_cast<float>(gs1) * inv_m;
+                    C = static_cast<float>(gs2) * inv_m;
+                }
+            }
+            dzc_s[sg][0][cl] = A; dzc_s[sg][1][cl] = Bc; dzc_s[sg][2][cl] = C;
+            dzc_s[sg][3][cl] = M; dzc_s[sg][4][cl] = I;
+        }
+        if (bid == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
+            // dgamma/dbeta of each BN batch (segment), as the dz launch's block 0
+            for (int c = tid; c < n; c += DW_NT) {
+                for (int sg = 0; sg < (two ? 2 : 1); ++sg) {
+                    double gs1, gs2;
+                    slot_sums(a.g_stats + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * n, n, c, gs1, gs2);
+                    atomicAdd(&a.dgamma[c], static_cast<float>(gs2));
+                    atomicAdd(&a.dbeta[c], static_cast<float>(gs1));
+                }
+            }
+        }
+        __syncthreads();
+    }
+    // dbias: folded from the dz launch's fp64 slots by block 0, or (no slots,
+    // or dz computed here) summed here by the k-tile-0 blocks
+    if (!DZF && a.dbias && a.dbias_slots && bid == 0) {
         for (int cc = tid; cc < n; cc += DW_NT) {
             double v = 0.0;
 #pragma unroll
@@ -1093,7 +1136,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
             atomicAdd(&a.dbias[cc], static_cast<float>(v));
         }
     }
-    const bool do_bias = a.dbias != nullptr && a.dbias_slots == nullptr && by == 0;
+    const bool do_bias = a.dbias != nullptr && (DZF || a.dbias_slots == nullptr) && by == 0;
 
     if (gather) {
         for (int64_t t = tid; t < r_end - r_begin; t += DW_NT) {
@@ -1103,14 +1146,25 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         __syncthreads();
     }
 
-    float4 rd[LN], ra[LK];  // one chunk's staged values (prefetch registers)
+    float4 rd[LN], rz[DZF ? LN : 1], ra[LK];  // one chunk's staged values (prefetch registers)
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float dsl = act_slope(a.act);
     auto load = [&](int64_t base) {
 #pragma unroll
         for (int j = 0; j < LN; ++j) {
             const int e = tid + DW_NT * j, row = e / VN;
             const int64_t r = base + row;
             float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (DZF) {  // g and z of the row (n % 4 == 0, checked by the host)
+                float4 zv = v;
+                if (e < DW_R * VN && r < r_end && gn < n) {
+                    v = *reinterpret_cast<const float4*>(a.g + r * n + gn);
+                    zv = *reinterpret_cast<const float4*>(a.z + r * n + gn);
+                }
+                rd[j] = v;
+                rz[j] = zv;
+                continue;
+            }
             if (e < DW_R * VN && r < r_end) {
                 const float* dz = a.dz_ws + r * n + gn;
                 if constexpr (VEC) {
@@ -1151,6 +1205,25 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         for (int j = 0; j < LN; ++j) {
             const int e = tid + DW_NT * j, row = e / VN;
             if (e < DW_R * VN) {
+                if constexpr (DZF) {
+                    // dz = A·(g − B − x̂·C)·act'(z), x̂ = (act(z) − M)·I (phase A of the dz launch)
+                    const int64_t r = base + row;
+                    const int sg = (two && r >= a.seg_split) ? 1 : 0;
+                    const bool ok = r < r_end;
+                    float4 d;
+                    auto one = [&](float g, float z, int i) {
+                        const int cl = cn + i;
+                        const float A = dzc_s[sg][0][cl], Bc = dzc_s[sg][1][cl], C = dzc_s[sg][2][cl];
+                        const float M = dzc_s[sg][3][cl], I = dzc_s[sg][4][cl];
+                        const float xh = (act_pwl(dsl, z) - M) * I;
+                        return (ok && gn + i < n) ? A * (g - Bc - xh * C) * (z > 0.f ? 1.f : dsl) : 0.f;
+                    };
+                    d.x = one(rd[j].x, rz[j].x, 0);
+                    d.y = one(rd[j].y, rz[j].y, 1);
+                    d.z = one(rd[j].z, rz[j].z, 2);
+                    d.w = one(rd[j].w, rz[j].w, 3);
+                    rd[j] = d;
+                }
                 *reinterpret_cast<float4*>(&Ld[buf][row * LDN + cn]) = rd[j];
                 bsum.x += rd[j].x; bsum.y += rd[j].y; bsum.z += rd[j].z; bsum.w += rd[j].w;
             }
@@ -1338,6 +1411,20 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
     return rt_linear_fwd_f32_multi(args, 1, stream);
 }
 
+// the dz launch of a dA-free layer (first Linear, no input gradient) folds into
+// its dW launch (rt_linear_bwd_args.fuse_dz): piecewise-linear activation,
+// BN modes 1-3, n % 4 == 0
+static bool dz_fusable(const rt_linear_bwd_args& a) {
+    return a.fuse_dz && !a.g_prev && !a.dsrc && a.grad_mode >= 1 && a.grad_mode <= 3 &&
+           act_is_piecewise_linear(a.act) && (a.n % 4) == 0 && a.g && a.z &&
+           (reinterpret_cast<uintptr_t>(a.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.z) & 15) == 0;
+}
+static bool all_dz_fusable(const rt_linear_bwd_args* args, int n_args) {
+    for (int g = 0; g < n_args; ++g)
+        if (!dz_fusable(args[g])) return false;
+    return true;
+}
+
 static int validate_bwd(const rt_linear_bwd_args* args) {
     if (!args) return RT_ERR_INVALID;
     const rt_linear_bwd_args& a = *args;
@@ -1375,6 +1462,7 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
         lds = l > lds ? l : lds;
         blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
     }
+    if (all_dz_fusable(args, n_args)) return RT_OK;  // dz computed by the dW launch
     mlp::BwdLaunch L{};
     L.a0 = args[0];
     L.a1 = n_args > 1 ? args[1] : args[0];
@@ -1389,6 +1477,10 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
         default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, L); break;
     }
     return check_launch("linear_bwd_dz_kernel");
+}
+
+extern "C" int rt_linear_bwd_dz_fused(const rt_linear_bwd_args* args, int n_args) {
+    return (args && n_args >= 1 && n_args <= 2 && all_dz_fusable(args, n_args)) ? 1 : 0;
 }
 
 extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream) {
@@ -1464,10 +1556,16 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     const dim3 grid(total);
     hipStream_t st = as_stream(stream);
     const bool vec = L.vec0 && L.vec1;
-#define RT_DW(BN, BK, P)                                                                                          \
-    do {                                                                                                          \
-        if (vec) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, true>), grid, dim3(mlp::DW_NT), 0, st, L);  \
-        else hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, false>), grid, dim3(mlp::DW_NT), 0, st, L);     \
+    const bool dzf = all_dz_fusable(args, n_args);
+#define RT_DW(BN, BK, P)                                                                                                 \
+    do {                                                                                                                 \
+        if (dzf) {                                                                                                       \
+            if (vec) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, true, true>), grid, dim3(mlp::DW_NT), 0, st, L);  \
+            else hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, false, true>), grid, dim3(mlp::DW_NT), 0, st, L);     \
+        } else {                                                                                                         \
+            if (vec) hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, true, false>), grid, dim3(mlp::DW_NT), 0, st, L); \
+            else hipLaunchKernelGGL((mlp::linear_bwd_dw_kernel<BN, BK, P, false, false>), grid, dim3(mlp::DW_NT), 0, st, L);    \
+        }                                                                                                                \
     } while (0)
     if (small_k) {
         switch (pro) { case 0: RT_DW(128, 32, 0); break; case 1: RT_DW(128, 32, 1); break;

@@ -413,8 +413,9 @@ def _launch_bwd(group: list, st) -> None:
     flops = sum((2.0 if d else 0.0) * a.m * a.k * a.n for a, d in zip(group, da))
     nbytes = sum(4.0 * (3 * a.m * a.n + (2 * a.m * a.k if d else 0) + a.n * a.k) for a, d in zip(group, da))
     arr = (LinearBwdArgs * len(group))(*group)
-    with TIMER.region("linear_bwd_dz", flops=flops, bytes_=nbytes):
-        call("rt_linear_bwd_dz_f32_multi", arr, len(group), st)
+    if not native.lib().rt_linear_bwd_dz_fused(arr, len(group)):  # else the dW launch computes dz
+        with TIMER.region("linear_bwd_dz", flops=flops, bytes_=nbytes):
+            call("rt_linear_bwd_dz_f32_multi", arr, len(group), st)
     with TIMER.region("linear_bwd_dw", flops=sum(2.0 * a.m * a.k * a.n for a in group),
                       bytes_=sum(4.0 * (a.m * a.n + a.m * a.k + a.n * a.k) for a in group)):
         call("rt_linear_bwd_dw_f32_multi", arr, len(group), st)
@@ -487,6 +488,8 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
                 a.dgamma = slab.grad_of(b.bn.weight).data_ptr()
                 a.dbeta = slab.grad_of(b.bn.bias).data_ptr()
         # input of this linear (recomputed by the same prologue as forward)
+        if li == 0 and not want_dsrc:
+            a.fuse_dz = 1  # no dA: the dW launch computes dz (the dz launch becomes a no-op)
         if li == 0:
             a.src = ctx.src.data_ptr()
             a.src_rows = ctx.src.shape[0]
