@@ -380,7 +380,7 @@ KERNEL_SOURCES = {
     "linear_bwd_dw": ["mlp.hip", "rt_common.h"], "loss_fwd_bwd": ["loss.hip", "rt_common.h"],
     "clip_adam": ["optim.hip", "rt_common.h"],
     "flatip_topk_c4": ["topk_api.hip", "topk_f16.hip", "topk_impl.h", "topk_v1.h", "topk_v2.h", "topk_v3.h",
-                       "rt_sort.h", "rt_common.h"],
+                       "topk_v4.h", "topk_dense.h", "rt_sort.h", "rt_common.h"],
 }
 
 

@@ -29,7 +29,8 @@ def _bench_module():
 FAMILY = {"linear_fwd_kernel": ["linear_fwd"], "linear_bwd_dz_kernel": ["linear_bwd_dz"],
           "linear_bwd_dw_kernel": ["linear_bwd_dw"], "loss_fwd_kernel": ["loss_fwd_bwd"],
           "loss_bwd_kernel": ["loss_fwd_bwd"], "clip_adam_kernel": ["clip_adam"],
-          "grad_sqnorm_kernel": ["clip_adam"], "flatip_topk_v2_kernel": ["flatip_topk_c4"]}
+          "grad_sqnorm_kernel": ["clip_adam"], "flatip_topk_v2_kernel": ["flatip_topk_c4"],
+          "flatip_topk_v4_scan": ["flatip_topk_c4"], "flatip_topk_v4_finish": ["flatip_topk_c4"]}
 
 
 def parse(path):
