@@ -206,13 +206,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     const bool fast = vec && (a.k % 4) == 0 && (256 % vpr) == 0 &&
                       (a.prev_mode == 0 || act_is_piecewise_linear(a.prev_act));
     const bool early = fast && !a.ids && 8 * (256 / vpr) >= FM;  // one pass covers the tile
-    // Wᵀ for the backward's dz launch (rt_linear_fwd_args.wt_out): blocks
-    // 0 .. tiles-1 of each group each copy one 32x32 tile of W, transposed
-    // (float4 reads along k, scattered 4-byte writes; 32 tiles at the C2 layer 2)
+    // Wᵀ for the backward's dz launch (rt_linear_fwd_args.wt_out): the blocks
+    // of each group copy its 32x32 tiles of W transposed, tile i on block
+    // i mod (the group's blocks) — a group may have fewer row blocks than W
+    // has tiles (32 tiles at the C2 layer 2; 8 row blocks for a batch of 256)
     if (a.wt_out) {
         const int tk = (k + 31) / 32, tiles = tk * ((n + 31) / 32);
-        if (static_cast<int>(bid) < tiles) {
-            const int n0 = (static_cast<int>(bid) / tk) * 32, k0 = (static_cast<int>(bid) % tk) * 32;
+        const int nblk = static_cast<int>(g1 ? gridDim.x - L.split : L.split);
+        for (int wt = static_cast<int>(bid); wt < tiles; wt += nblk) {
+            const int n0 = (wt / tk) * 32, k0 = (wt % tk) * 32;
             const int r = tid >> 3, c = (tid & 7) * 4;
             if (n0 + r < n) {
 #pragma unroll
