@@ -413,7 +413,9 @@ def _launch_bwd(group: list, st) -> None:
     flops = sum((2.0 if d else 0.0) * a.m * a.k * a.n for a, d in zip(group, da))
     nbytes = sum(4.0 * (3 * a.m * a.n + (2 * a.m * a.k if d else 0) + a.n * a.k) for a, d in zip(group, da))
     arr = (LinearBwdArgs * len(group))(*group)
-    if not native.lib().rt_linear_bwd_dz_fused(arr, len(group)):  # else the dW launch computes dz
+    lib = native.lib()
+    fused = hasattr(lib, "rt_linear_bwd_dz_fused") and lib.rt_linear_bwd_dz_fused(arr, len(group))
+    if not fused:  # else the dW launch computes dz (older library builds: always the dz launch)
         with TIMER.region("linear_bwd_dz", flops=flops, bytes_=nbytes):
             call("rt_linear_bwd_dz_f32_multi", arr, len(group), st)
     with TIMER.region("linear_bwd_dw", flops=sum(2.0 * a.m * a.k * a.n for a in group),
