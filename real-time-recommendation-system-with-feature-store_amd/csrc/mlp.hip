@@ -1704,6 +1704,9 @@ extern "C" int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream) {
 // its dW launch (rt_linear_bwd_args.fuse_dz): piecewise-linear activation,
 // BN modes 1-3, n % 4 == 0
 static bool dz_fusable(const rt_linear_bwd_args& a) {
+#ifdef RT_NO_DZ_FUSE  // A/B variant: always the separate dz launch
+    return false;
+#endif
     return a.fuse_dz && !a.g_prev && !a.dsrc && a.grad_mode >= 1 && a.grad_mode <= 3 &&
            act_is_piecewise_linear(a.act) && (a.n % 4) == 0 && a.g && a.z &&
            (reinterpret_cast<uintptr_t>(a.g) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.z) & 15) == 0;
