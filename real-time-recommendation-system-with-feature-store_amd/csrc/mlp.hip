@@ -572,241 +572,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 }
 
 // ---------------------------------------------------------------------------
-// forward, pipelined (layers without a row gather: C2 layers 2 and 3)
-// ---------------------------------------------------------------------------
-// One block per CU (the launch asks for enough LDS that no second block fits)
-// walks the row tiles t = bid, bid + blocks, ... of its group. With one block
-// per 32-row tile (linear_fwd_kernel) every block of a launch loads its A tile,
-// runs its MFMAs and stores in lockstep with the others, so the loads and the
-// MFMA pipe take turns; here the A tile of the next tile is requested before
-// the MFMAs of the current one, the BatchNorm of the previous block is
-// finalised once per block (both row segments), and the first W fragments are
-// loaded once. Same math as the fast paths of linear_fwd_kernel (same prologue
-// transform, k order, epilogues), so outputs are identical.
-//   L2OUT = false: hidden layer, z_out + fp64 BN column sums of act(z)
-//   L2OUT = true : final layer, row L2-normalised l2_out + norms_out
-template <bool L2OUT>
-__global__ __launch_bounds__(256) void linear_fwd_pipe_kernel(FwdLaunch L) {
-    const bool g1 = blockIdx.x >= L.split;
-    const rt_linear_fwd_args& a = g1 ? L.a1 : L.a0;
-    const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
-    const unsigned nblk = g1 ? gridDim.x - L.split : L.split;
-    extern __shared__ __attribute__((aligned(16))) float sm[];
-    const int k = a.k, n = a.n;
-    const int kp = pad8(k), kh = kp / 2, lda = kp + 4;
-    float* scale = sm;                 // [2][kp] per row segment
-    float* shift = scale + 2 * kp;     // [2][kp]
-    float* As = shift + 2 * kp;        // [FM][lda]
-    float* rowpart = As + FM * lda;    // [FM]
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int64_t m = a.m;
-    const int64_t tiles = m / FM;  // m % FM == 0 (host)
-    const bool two = a.seg_split > 0;
-    if (blockIdx.x == 0 && a.zero_buf)
-        for (int64_t e = tid; e < a.zero_words; e += 256) a.zero_buf[e] = 0.0;
-    if (a.wt_out) {  // Wᵀ for the backward's dz launch, as linear_fwd_kernel
-        const int tk = (k + 31) / 32, wtiles = tk * ((n + 31) / 32);
-        for (int wt = static_cast<int>(bid); wt < wtiles; wt += static_cast<int>(nblk)) {
-            const int n0 = (wt / tk) * 32, k0 = (wt % tk) * 32;
-            const int r = tid >> 3, c = (tid & 7) * 4;
-            if (n0 + r < n) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (k0 + c + j < k)
-                        a.wt_out[static_cast<int64_t>(k0 + c + j) * n + n0 + r] =
-                            a.w[static_cast<int64_t>(n0 + r) * k + k0 + c + j];
-            }
-        }
-    }
-    // W: wave w owns output columns w*32 .. w*32+31 (n <= 128)
-    const bool tile_on = w * 32 < n;
-    const int nn = w * 32 + c32;
-    const bool row_ok = nn < n;
-    const float* wrow = a.w + static_cast<int64_t>(row_ok ? nn : 0) * k;
-    auto load_w = [&](int s, float4 (&dst)[4]) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int kk = h * kh + s + 4 * j;
-            dst[j] = (tile_on && row_ok && kk < k) ? *reinterpret_cast<const float4*>(wrow + kk)
-                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    float4 wfirst[4];
-    load_w(0, wfirst);
-    // A tile loads: 4 fixed columns per thread, rows r0 + 4u (vpr = kp/4 <= 64)
-    const int vpr = kp / 4, rstep = 256 / vpr;
-    const int ca = (tid % vpr) * 4, ra = tid / vpr;
-    float4 pre[8];
-    auto load_a = [&](int64_t t) {
-        const int64_t row0 = t * FM;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int r = ra + u * rstep;
-            pre[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (r < FM && ca < k) pre[u] = *reinterpret_cast<const float4*>(a.src + (row0 + r) * a.ld_src + ca);
-        }
-    };
-    int64_t t = bid;
-    if (t < tiles) load_a(t);
-    // BatchNorm of the previous block, every segment, once per block (block 0
-    // owns the save / running-stat writes, in segment order)
-    const int nseg = two ? 2 : 1;
-    if (a.prev_mode == 1 || a.prev_mode == 2) {
-        for (int c = tid; c < k; c += 256) {
-            for (int sg = 0; sg < nseg; ++sg) {
-                const int64_t ms = two ? (sg == 0 ? a.seg_split : m - a.seg_split) : m;
-                float mean, invstd, var_f = 0.f;
-                if (a.prev_mode == 1) {
-                    double s1, s2;
-                    slot_sums(a.prev_stats + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * k, k, c, s1, s2);
-                    const double md = s1 / static_cast<double>(ms);
-                    double vd = s2 / static_cast<double>(ms) - md * md;
-                    vd = vd > 0.0 ? vd : 0.0;
-                    mean = static_cast<float>(md);
-                    invstd = static_cast<float>(1.0 / sqrt(vd + static_cast<double>(a.bn_eps)));
-                    var_f = static_cast<float>(ms > 1 ? vd * static_cast<double>(ms) / static_cast<double>(ms - 1) : vd);
-                } else {
-                    mean = a.running_mean[c];
-                    invstd = static_cast<float>(1.0 / sqrt(static_cast<double>(a.running_var[c]) + a.bn_eps));
-                }
-                bn_affine(a.bn_gamma[c], a.bn_beta[c], mean, invstd, scale[sg * kp + c], shift[sg * kp + c]);
-                if (blockIdx.x == 0 || (g1 && bid == 0)) {
-                    if (c == 0 && a.prev_mode == 1 && a.num_batches_tracked) *a.num_batches_tracked += 1;
-                    if (a.save_mean) a.save_mean[sg * k + c] = mean;
-                    if (a.save_invstd) a.save_invstd[sg * k + c] = invstd;
-                    if (a.prev_mode == 1 && a.running_mean) {
-                        const float mo = a.bn_momentum;
-                        a.running_mean[c] = (1.f - mo) * a.running_mean[c] + mo * mean;
-                        a.running_var[c] = (1.f - mo) * a.running_var[c] + mo * var_f;
-                    }
-                }
-            }
-        }
-    }
-    __syncthreads();
-    const uint64_t seed = a.drop_seed + (a.seed_offset ? *a.seed_offset : 0ull);
-    const bool bn = a.prev_mode == 1 || a.prev_mode == 2;
-    const float psl = act_slope(a.prev_act);
-    const bool drop = a.drop_p > 0.f && a.prev_mode != 0;
-    const float dscale = a.drop_p > 0.f ? 1.f / (1.f - a.drop_p) : 1.f;
-    const float bcol = (row_ok && a.bias) ? a.bias[nn] : 0.f;
-    const float asl = act_slope(a.act);
-    for (; t < tiles; t += nblk) {
-        const int64_t row0 = t * FM;
-        const int seg = (two && row0 >= a.seg_split) ? 1 : 0;
-        {   // stage the transformed A tile (the prologue of linear_fwd_kernel's fast path)
-            const float4 sc4 = bn ? *reinterpret_cast<const float4*>(scale + seg * kp + ca) : make_float4(1.f, 1.f, 1.f, 1.f);
-            const float4 sh4 = bn ? *reinterpret_cast<const float4*>(shift + seg * kp + ca) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int r = ra + u * rstep;
-                if (r >= FM) break;
-                const int64_t gr = row0 + r;
-                auto tf = [&](float x, int cc, float scv, float shv) {
-                    if (a.prev_mode == 0) return x;
-                    x = act_pwl(psl, x);
-                    if (bn) x = __builtin_fmaf(x, scv, shv);
-                    if (drop) x = dropout_keep(seed, gr, cc, a.drop_p) ? x * dscale : 0.f;
-                    return x;
-                };
-                float4 o;
-                const bool ok = ca < k;
-                o.x = ok ? tf(pre[u].x, ca, sc4.x, sh4.x) : 0.f;
-                o.y = ok ? tf(pre[u].y, ca + 1, sc4.y, sh4.y) : 0.f;
-                o.z = ok ? tf(pre[u].z, ca + 2, sc4.z, sh4.z) : 0.f;
-                o.w = ok ? tf(pre[u].w, ca + 3, sc4.w, sh4.w) : 0.f;
-                *reinterpret_cast<float4*>(As + r * lda + ca) = o;
-            }
-        }
-        __syncthreads();
-        if (t + nblk < tiles) load_a(t + nblk);  // the next tile's rows land during the MFMAs below
-        f32x16 acc = f32x16{};
-        const float* ap = As + c32 * lda + h * kh;
-        float4 wv[4], wn[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wn[j] = wfirst[j];
-        for (int s = 0; s < kh; s += 16) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) wv[j] = wn[j];
-            if (s + 16 < kh) load_w(s + 16, wn);
-            float4 av[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) av[j] = *reinterpret_cast<const float4*>(ap + s + 4 * j);
-            if (tile_on) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc = mfma(av[j].x, wv[j].x, acc);
-                    acc = mfma(av[j].y, wv[j].y, acc);
-                    acc = mfma(av[j].z, wv[j].z, acc);
-                    acc = mfma(av[j].w, wv[j].w, acc);
-                }
-            }
-        }
-        if constexpr (!L2OUT) {
-            // hidden layer: z (write-through) and the fp64 column sums of act(z)
-            double* const stats = a.stats_out ? a.stats_out + (static_cast<int64_t>(seg) * RT_STAT_SLOTS +
-                                                               t % RT_STAT_SLOTS) * 2 * n : nullptr;
-            if (tile_on) {
-                float s1 = 0.f, s2 = 0.f;
-                float* zp = a.z_out + (row0 + 4 * h) * n + nn;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float z = acc[r] + bcol;
-                    if (row_ok) st_act(zp + ((r & 3) + 8 * (r >> 2)) * n, z);
-                    const float av = act_pwl(asl, z);
-                    s1 += av;
-                    s2 += av * av;
-                }
-                if (!row_ok) s1 = s2 = 0.f;
-                s1 += __shfl_xor(s1, 32, 64);
-                s2 += __shfl_xor(s2, 32, 64);
-                if (stats && h == 0 && row_ok) {
-                    atomicAdd(&stats[nn], static_cast<double>(s1));
-                    atomicAdd(&stats[n + nn], static_cast<double>(s2));
-                }
-            }
-            __syncthreads();  // every wave is done reading As before the next tile is staged
-        } else {
-            // final layer: the fast L2-normalise epilogue of linear_fwd_kernel
-            __syncthreads();  // every wave is done reading As
-            float* zsq = As;  // [n][FM + 1]
-            if (tile_on) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const float z = acc[r] + bcol;
-                    acc[r] = z;
-                    if (row_ok) zsq[nn * (FM + 1) + lr] = z * z;
-                }
-            }
-            __syncthreads();
-            {
-                const int row = tid >> 3, part = tid & 7;
-                float ss = 0.f;
-                for (int c = part; c < n; c += 8) ss += zsq[c * (FM + 1) + row];
-                ss += __shfl_xor(ss, 1, 64);
-                ss += __shfl_xor(ss, 2, 64);
-                ss += __shfl_xor(ss, 4, 64);
-                if (part == 0) {
-                    const float nrm = sqrtf(ss);
-                    rowpart[row] = 1.f / fmaxf(nrm, kNormEps);
-                    if (a.norms_out) a.norms_out[row0 + row] = nrm;
-                }
-            }
-            __syncthreads();
-            if (tile_on && row_ok) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int lr = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    st_act(a.l2_out + (row0 + lr) * n + nn, acc[r] * rowpart[lr]);
-                }
-            }
-            __syncthreads();  // zsq / rowpart reads done before the next tile is staged
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // backward 1: dz, dgamma/dbeta, dA = dz·W (+ g_prev / dsrc epilogue)
 // ---------------------------------------------------------------------------
 // Block = 32 rows. dz (32 x n) lives in LDS; dA = dz·W reads W[n][k] rows
@@ -1602,26 +1367,6 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
     return RT_OK;
 }
 
-// the pipelined forward's launch: one 256-thread block per CU, made sure of by
-// its LDS request (two would not fit in 160 KiB)
-constexpr int kPipeBlocks = 256;
-constexpr size_t kPipeLds = 96 * 1024;
-
-// 0 / 1: this Linear fits linear_fwd_pipe_kernel<false / true>; -1: it does not
-static int fwd_pipe_kind(const rt_linear_fwd_args& a) {
-    const int kp = mlp::pad8(a.k);
-    if (a.ids || a.n > 128 || (a.k % 4) != 0 || (a.ld_src % 4) != 0 || (256 % (kp / 4)) != 0 || kp > 256) return -1;
-    if ((reinterpret_cast<uintptr_t>(a.src) | reinterpret_cast<uintptr_t>(a.w)) & 15) return -1;
-    if (a.prev_mode != 0 && !act_is_piecewise_linear(a.prev_act)) return -1;
-    if (a.m % mlp::FM != 0 || a.m == 0) return -1;
-    const size_t need = (4 * static_cast<size_t>(kp) + mlp::FM * (kp + 4) + mlp::FM) * sizeof(float);
-    if (need > kPipeLds) return -1;
-    if (a.l2_out && !a.z_out && !a.stats_out && static_cast<size_t>(a.n) * (mlp::FM + 1) <= mlp::FM * (kp + 4))
-        return 1;
-    if (!a.l2_out && a.z_out && act_is_piecewise_linear(a.act)) return 0;
-    return -1;
-}
-
 extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_args, void* stream) {
     if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
     int tpw = 1, kp_max = 0;
@@ -1649,38 +1394,6 @@ extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_arg
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
     if (total == 0) return RT_OK;
     hipStream_t st = as_stream(stream);
-#ifndef RT_NO_FWD_PIPE
-    // pipelined persistent form: one block per CU over the row tiles of its group
-    {
-        int l2 = -1;
-        bool ok = true;
-        for (int g = 0; g < n_args && ok; ++g) {
-            const int v = fwd_pipe_kind(args[g]);
-            ok = v >= 0 && (l2 < 0 || v == l2);
-            l2 = v;
-        }
-        if (ok && total > static_cast<unsigned>(kPipeBlocks)) {
-            unsigned nb0 = blocks[0], nb1 = n_args > 1 ? blocks[1] : 0u;
-            const double tot = static_cast<double>(nb0 + nb1);
-            unsigned p0 = static_cast<unsigned>(kPipeBlocks * (nb0 / tot) + 0.5);
-            if (p0 < 1) p0 = 1;
-            if (n_args > 1 && p0 > static_cast<unsigned>(kPipeBlocks) - 1) p0 = kPipeBlocks - 1;
-            unsigned p1 = n_args > 1 ? kPipeBlocks - p0 : 0u;
-            if (p0 > nb0) p0 = nb0;
-            if (p1 > nb1) p1 = nb1;
-            L.split = p0;
-            const size_t plds = kPipeLds;
-            if (l2) {
-                allow_lds(mlp::linear_fwd_pipe_kernel<true>, plds);
-                hipLaunchKernelGGL(mlp::linear_fwd_pipe_kernel<true>, dim3(p0 + p1), dim3(256), plds, st, L);
-            } else {
-                allow_lds(mlp::linear_fwd_pipe_kernel<false>, plds);
-                hipLaunchKernelGGL(mlp::linear_fwd_pipe_kernel<false>, dim3(p0 + p1), dim3(256), plds, st, L);
-            }
-            return check_launch("linear_fwd_pipe_kernel");
-        }
-    }
-#endif
     const dim3 grid(total);
 #define RT_FWD(T, V)                                                                              \
     do {                                                                                          \
