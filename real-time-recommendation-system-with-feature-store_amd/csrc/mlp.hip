@@ -1040,7 +1040,10 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     static_assert(2 * DW_R * LDK >= (DW_NT / 64) * VN * 4, "dbias partials fit in the A buffers");
     __shared__ __attribute__((aligned(16))) float Ld[2][DW_R * LDN];
     __shared__ __attribute__((aligned(16))) float La[2][DW_R * LDK];
-    __shared__ int srow[DW_MAXR];
+    // gather ids staged for the first Linear only (PRO 0): the other instances
+    // stay at <= 53 KB of LDS, 3 blocks per CU (the C2 layer-2 dW launch's ~750
+    // blocks then run as one wave of blocks instead of two)
+    __shared__ int srow[PRO == 0 ? DW_MAXR : 1];
     __shared__ __attribute__((aligned(16))) float aff_s[2][2][BK];  // [segment][scale, shift][tile column]
     __shared__ __attribute__((aligned(16))) float dzc_s[DZF ? 2 : 1][5][DZF ? BN : 4];  // DZF: [seg][A,B,C,M,I][col]
 
@@ -1059,7 +1062,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
     if (r_begin >= m) return;  // a padding split (block-uniform, before any barrier)
     RT_PP_DECL
-    const bool gather = a.ids != nullptr;
+    const bool gather = PRO == 0 && a.ids != nullptr;  // (the host refuses ids with a transformed input)
     const bool two = a.seg_split > 0;
 
     // staging columns of this thread (the same for every staged row)
@@ -1526,6 +1529,7 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     for (int g = 0; g < n_args; ++g) {
         const int v = validate_bwd(&args[g]);
         if (v) return v;
+        if (args[g].ids && args[g].prev_mode != 0) return RT_ERR_UNSUPPORTED;  // a gather feeds the first Linear only
         small_k = small_k && args[g].k <= 32;
     }
     for (int g = 0; g < n_args; ++g) {
