@@ -1495,29 +1495,43 @@ extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream
     return rt_linear_bwd_dz_f32_multi(args, 1, stream);
 }
 
-// dW tiling of one Linear: 64x64 tiles (128x32 when k <= 32), ~512 blocks
-// (2 per CU), whole 32-row chunks, <= 64 splits per tile (128 when k <= 32;
-// float atomics per dW element), <= DW_MAXR rows per split (gather ids staged
-// in LDS)
-static void dw_plan(const rt_linear_bwd_args& a, bool small_k, unsigned& tn, unsigned& tk, int64_t& splits,
-                    int64_t& rps) {
+// dW tiling of one launch (one or two Linears): 64x64 tiles (128x32 when
+// k <= 32), whole 32-row chunks, ONE rows-per-split for both groups so that
+// every block carries the same work (round 3 split each group for ~512 blocks
+// of its own: the user tower's 1,024 rows went out as 32-row blocks that each
+// added a whole tile with atomics). About RT_DW_BLOCKS blocks (tiles x row
+// splits; each block adds one tile with fp32 atomics, so atomic bytes =
+// blocks x tile); <= 64 splits per group (128 when k <= 32); <= DW_MAXR rows
+// per split (gather ids staged in LDS). A/B at C2 (profiles/r04_c2_ab_dw_plan.txt):
+// 384 / 512 / 768 blocks within 1 µs of each other, 2-2.5 µs/step under the
+// per-group plan; an XCD-contiguous block order (the tiles of a split on one
+// XCD, sharing its L2) was 7 µs/step SLOWER and is not used.
+#ifndef RT_DW_BLOCKS
+#define RT_DW_BLOCKS 384
+#endif
+#ifndef RT_DW_BLOCKS_SMALLK
+#define RT_DW_BLOCKS_SMALLK 256
+#endif
+static void dw_plan(const rt_linear_bwd_args* args, int n_args, bool small_k, unsigned* tn, unsigned* tk,
+                    int64_t* splits, int64_t& rps) {
     const int bn = small_k ? 128 : 64, bk = small_k ? 32 : 64;
-    tn = static_cast<unsigned>((a.n + bn - 1) / bn);
-    tk = static_cast<unsigned>((a.k + bk - 1) / bk);
-    const int64_t tiles = static_cast<int64_t>(tn) * tk;
-    splits = (512 + tiles - 1) / tiles;
-    // a k <= 32 layer (C2 layer 1: 2 tiles) has too little work per row for 64
-    // splits to fill the chip: cap 128 measured 6 µs/step faster than 64 (256:
-    // 4.5 µs faster, 576: 14 µs slower)
     const int64_t cap = small_k ? 128 : 64;
-    if (splits > cap) splits = cap;
-    const int64_t max_splits = (a.m + mlp::DW_R - 1) / mlp::DW_R;
-    if (splits > max_splits) splits = max_splits;
-    if (splits < 1) splits = 1;
-    rps = (a.m + splits - 1) / splits;
+    int64_t work = 0, rmin = mlp::DW_R;
+    for (int g = 0; g < n_args; ++g) {
+        const rt_linear_bwd_args& a = args[g];
+        tn[g] = static_cast<unsigned>((a.n + bn - 1) / bn);
+        tk[g] = static_cast<unsigned>((a.k + bk - 1) / bk);
+        work += a.m * tn[g] * tk[g];
+        const int64_t r = (a.m + cap - 1) / cap;
+        rmin = r > rmin ? r : rmin;
+    }
+    const int64_t target = small_k ? RT_DW_BLOCKS_SMALLK : RT_DW_BLOCKS;
+    rps = (work + target - 1) / target;
+    rps = rps > rmin ? rps : rmin;
     rps = (rps + mlp::DW_R - 1) / mlp::DW_R * mlp::DW_R;
-    if (a.ids && rps > mlp::DW_MAXR) rps = mlp::DW_MAXR;
-    splits = (a.m + rps - 1) / rps;
+    for (int g = 0; g < n_args; ++g)
+        if (args[g].ids && rps > mlp::DW_MAXR) rps = mlp::DW_MAXR;
+    for (int g = 0; g < n_args; ++g) splits[g] = args[g].m > 0 ? (args[g].m + rps - 1) / rps : 0;
 }
 
 extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream) {
@@ -1532,16 +1546,16 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
         if (args[g].ids && args[g].prev_mode != 0) return RT_ERR_UNSUPPORTED;  // a gather feeds the first Linear only
         small_k = small_k && args[g].k <= 32;
     }
+    unsigned tns[2] = {1u, 1u}, tks[2] = {1u, 1u};
+    int64_t nsplit[2] = {0, 0}, rps = mlp::DW_R;
+    dw_plan(args, n_args, small_k, tns, tks, nsplit, rps);
     for (int g = 0; g < n_args; ++g) {
         const rt_linear_bwd_args& a = args[g];
-        unsigned tn = 0, tk = 0;
-        int64_t splits = 0, rps = 0;
-        if (a.m > 0) dw_plan(a, small_k, tn, tk, splits, rps);
-        const int64_t nb = static_cast<int64_t>(tn) * tk * splits;
+        const int64_t nb = static_cast<int64_t>(tns[g]) * tks[g] * nsplit[g];
         if (nb > (1ll << 30)) return RT_ERR_UNSUPPORTED;
         blocks[g] = static_cast<unsigned>(nb);
-        (g ? L.tn1 : L.tn0) = tn ? tn : 1u;
-        (g ? L.tk1 : L.tk0) = tk ? tk : 1u;
+        (g ? L.tn1 : L.tn0) = tns[g] ? tns[g] : 1u;
+        (g ? L.tk1 : L.tk0) = tks[g] ? tks[g] : 1u;
         (g ? L.rps1 : L.rps0) = rps;
         int p = 0;
         if (a.prev_mode != 0) p = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
