@@ -119,6 +119,56 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// ---- fp32 products on the bf16 MFMA (three-piece split) ----
+// x = hi + mid + lo with each piece the RNE bf16 of what the previous pieces
+// left (every residual is exact in fp32), |x - hi - mid - lo| <= 2^-24 |x|.
+// A product x·y is taken as the 6 piece products of order <= 2^-16 (hi·hi,
+// hi·mid, mid·hi, mid·mid, hi·lo, lo·hi); the 3 dropped ones are below
+// 2^-23 |x·y|, and each piece product is exact in the MFMA's fp32 sum. So a
+// 32x32x16 bf16 MFMA sextet does the work of 8 fp32 32x32x2 MFMAs at 6 x 32
+// instead of 8 x 64 cycles, with fp32-class error (the sum order differs from
+// the fp32 MFMA's, as any blocked fp32 GEMM's does).
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma_bf16(s16x8 a, s16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(__attribute__((ext_vector_type(8))) __bf16, a),
+                                                   __builtin_bit_cast(__attribute__((ext_vector_type(8))) __bf16, b),
+                                                   c, 0, 0, 0);
+}
+struct Pieces {
+    s16x8 hi, mid, lo;
+};
+// (x0, x1) → the three piece pairs, element x0 in the low half of each dword
+__device__ __forceinline__ void split3(float x0, float x1, uint32_t& h, uint32_t& m, uint32_t& l) {
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    h = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{x0, x1}, b2));
+    float r0 = x0 - __builtin_bit_cast(float, h << 16), r1 = x1 - __builtin_bit_cast(float, h & 0xffff0000u);
+    m = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{r0, r1}, b2));
+    r0 -= __builtin_bit_cast(float, m << 16);
+    r1 -= __builtin_bit_cast(float, m & 0xffff0000u);
+    l = __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{r0, r1}, b2));
+}
+__device__ __forceinline__ Pieces split8(const float (&x)[8]) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    u4 h, m, l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t a, b, c;
+        split3(x[2 * j], x[2 * j + 1], a, b, c);
+        h[j] = a; m[j] = b; l[j] = c;
+    }
+    return Pieces{__builtin_bit_cast(s16x8, h), __builtin_bit_cast(s16x8, m), __builtin_bit_cast(s16x8, l)};
+}
+// acc += A·B over one 16-deep k-block, small products first
+__device__ __forceinline__ f32x16 mfma3(const Pieces& a, const Pieces& b, f32x16 c) {
+    c = mfma_bf16(a.lo, b.hi, c);
+    c = mfma_bf16(a.hi, b.lo, c);
+    c = mfma_bf16(a.mid, b.mid, c);
+    c = mfma_bf16(a.mid, b.hi, c);
+    c = mfma_bf16(a.hi, b.mid, c);
+    return mfma_bf16(a.hi, b.hi, c);
+}
+
 // previous-block transform applied to every A element (forward AND backward
 // recompute use this one function, so the recomputed A is bit-identical)
 struct Pro {
@@ -586,7 +636,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
-    const int np = pad8(n), nh = np / 2, ldz = np + 4;
+    const int np = pad8(n), ldz = np + 4;
     float* Dz = sm;  // [FM][ldz]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
     const int64_t row0 = static_cast<int64_t>(bid) * FM;
@@ -596,8 +646,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     RT_PP_DECL
 
     // one-tile waves request dA's first W fragments here, ahead of phase A
-    // (they do not depend on it), so their latency hides behind the dz tile
-    // 8 k-steps per iteration (nh % 16 == 0); next iteration's W loaded during this one's MFMAs
+    // (they do not depend on it), so their latency hides behind the dz tile.
+    // One 16-deep k-block (bf16 MFMA sextet) per iteration: lane half h holds
+    // n = kb + 8h .. kb + 8h + 7; the next k-block's W loaded during this one's MFMAs
     float wv[TPWK][8], wn[TPWK][8];
     // (the W pointer read once: inside the conditional loads below a field of
     // the selected launch group was re-loaded from the kernarg segment per load)
@@ -615,7 +666,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             const int kk = (w + 4 * i) * 32 + c32;
             const bool on = (w + 4 * i) * 32 < k && kk < k;
             if (WtT) {
-                const int nn = h * nh + s;
+                const int nn = s + 8 * h;
                 float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
                 if (on && nn < n) {
                     const float* p = WtT + static_cast<int64_t>(kk) * n + nn;
@@ -627,7 +678,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const int nn = h * nh + s + j;
+                    const int nn = s + 8 * h + j;
                     dst[i][j] = (on && nn < n) ? Wt[static_cast<int64_t>(nn) * k + kk] : 0.f;
                 }
             }
@@ -875,11 +926,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     __syncthreads();
     RT_PP_MARK(1)
 
-    // ---- phase B: dA = dz · W  (reduction over n, permuted per lane half) ----
+    // ---- phase B: dA = dz · W on the bf16 MFMA (three-piece split) ----
+    // the dz tile's pieces go to LDS once per block ([3][FM][ldb] bf16, rows
+    // padded by 16 B: the 32 rows of a ds_read_b128 cover the 64 banks); W's
+    // are split in registers per k-block
+    const int ldb = np + 8;
+    uint16_t* const planes = reinterpret_cast<uint16_t*>(Dz + FM * ldz + 5 * np);
+    const int plane = FM * ldb;
+    for (int e = tid; e < FM * (np / 4); e += 256) {
+        const int r = e / (np / 4), c = (e - r * (np / 4)) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(Dz + r * ldz + c);
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3(v.x, v.y, h0, m0, l0);
+        split3(v.z, v.w, h1, m1, l1);
+        uint16_t* q = planes + r * ldb + c;
+        *reinterpret_cast<uint2*>(q) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(q + plane) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(q + 2 * plane) = make_uint2(l0, l1);
+    }
+    __syncthreads();
     f32x16 acc[TPWK];
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) acc[i] = f32x16{};
-    const float* dp = Dz + c32 * ldz + h * nh;
+    const uint16_t* ap = planes + c32 * ldb + 8 * h;
     const bool want_stats = a.g_prev && a.g_prev_stats && (a.prev_mode == 1 || a.prev_mode == 2);
     // fast epilogue (the C2 hidden layers): a full row block, g_prev only, a
     // piecewise-linear previous activation — no per-element predicates, 32-bit
@@ -898,26 +967,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
         for (int r = 0; r < 16; ++r) zpre[i][r] = ld ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
     }
     if constexpr (TPWK != 1) load_w(0, wn);
-    for (int s = 0; s < nh; s += 8) {
+    for (int s = 0; s < np; s += 16) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i)
 #pragma unroll
             for (int j = 0; j < 8; ++j) wv[i][j] = wn[i][j];
-        if (s + 8 < nh) load_w(s + 8, wn);
-        float4 av[2];
-        av[0] = *reinterpret_cast<const float4*>(dp + s);
-        av[1] = *reinterpret_cast<const float4*>(dp + s + 4);
+        if (s + 16 < np) load_w(s + 16, wn);
+        Pieces pa;
+        pa.hi = *reinterpret_cast<const s16x8*>(ap + s);
+        pa.mid = *reinterpret_cast<const s16x8*>(ap + plane + s);
+        pa.lo = *reinterpret_cast<const s16x8*>(ap + 2 * plane + s);
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
             if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
-            acc[i] = mfma(av[0].x, wv[i][0], acc[i]);
-            acc[i] = mfma(av[0].y, wv[i][1], acc[i]);
-            acc[i] = mfma(av[0].z, wv[i][2], acc[i]);
-            acc[i] = mfma(av[0].w, wv[i][3], acc[i]);
-            acc[i] = mfma(av[1].x, wv[i][4], acc[i]);
-            acc[i] = mfma(av[1].y, wv[i][5], acc[i]);
-            acc[i] = mfma(av[1].z, wv[i][6], acc[i]);
-            acc[i] = mfma(av[1].w, wv[i][7], acc[i]);
+            acc[i] = mfma3(pa, split8(wv[i]), acc[i]);
         }
     }
     RT_PP_MARK(2)
@@ -1466,7 +1529,8 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
         const int t = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
         tpwk = t > tpwk ? t : tpwk;
         const int np = mlp::pad8(a.n);
-        const size_t l = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) + 16;
+        const size_t l = (static_cast<size_t>(mlp::FM) * (np + 4) + 5 * static_cast<size_t>(np)) * sizeof(float) +
+                         3 * static_cast<size_t>(mlp::FM) * (np + 8) * sizeof(uint16_t) + 16;
         lds = l > lds ? l : lds;
         blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
     }
