@@ -218,13 +218,13 @@ __device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, f
 // forward
 // ---------------------------------------------------------------------------
 // Block = 32 rows x all n columns; the transformed A tile (32 x k) lives in LDS
-// for the whole reduction (A fragments by ds_read_b128), W fragments stream
-// straight from L2 (float4 per lane per 4 MFMAs). The reduction index is
-// permuted (lane half h covers k in [h*kh, h*kh+kh)) so each lane's operands
-// are contiguous; 4 waves split the output columns.
+// as its three bf16 pieces for the whole reduction (A fragments by
+// ds_read_b128), W fragments stream straight from L2 (two float4 per lane per
+// k-block) and are split in registers; each 16-deep k-block is one bf16 MFMA
+// sextet (mfma3); 4 waves split the output columns.
 constexpr int FM = 32;  // rows per block
 
-__host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // kh % 16 == 0
+__host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // k padded to whole 32-deep iterations
 
 template <int TPW, bool KVEC>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 2))) void linear_fwd_kernel(FwdLaunch L) {
@@ -234,12 +234,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     constexpr int NT = 4 * TPW;  // column tiles in the block
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int k = a.k, n = a.n;
-    const int kp = pad8(k), kh = kp / 2, lda = kp + 4;
+    const int kp = pad8(k), aplane = FM * kp, aw = 3 * aplane / 2;
+    // 16-B chunk c of row r sits at chunk c ^ (r & am): the 32 rows of a
+    // ds_read_b128 then cover the 64 banks without padding (with a 16-B pad
+    // per row the k = 256 tile took 54 KB and 2 blocks per CU instead of 3)
+    const int nch = kp / 8, am = ((nch & -nch) < 16 ? (nch & -nch) : 16) - 1;
     float* scale = sm;                   // [kp]
     float* shift = scale + kp;           // [kp]
-    float* As = shift + kp;              // [FM][lda]
-    float* rowpart = As + FM * lda;      // [NT][FM]
+    float* As = shift + kp;              // A tile as three bf16 planes [3][FM][kp], chunk-swizzled (aw floats)
+    uint16_t* const Ap = reinterpret_cast<uint16_t*>(As);
+    float* rowpart = As + aw;            // [NT][FM]
     int64_t* srow = reinterpret_cast<int64_t*>(rowpart + NT * FM);  // [FM]
+    // the transformed A values go to LDS as their three bf16 pieces (split3)
+    auto put_a = [&](int r, int c, float4 o) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3(o.x, o.y, h0, m0, l0);
+        split3(o.z, o.w, h1, m1, l1);
+        uint16_t* q = Ap + r * kp + ((((c >> 3) ^ (r & am)) << 3) | (c & 7));
+        *reinterpret_cast<uint2*>(q) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(q + aplane) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(q + 2 * aplane) = make_uint2(l0, l1);
+    };
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
     const int64_t row0 = static_cast<int64_t>(bid) * FM;
@@ -285,7 +300,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
         row_ok[i] = nn < n;
         wrow[i] = a.w + static_cast<int64_t>(row_ok[i] ? nn : 0) * k;
     }
-    // 16 k-steps per iteration (kh % 16 == 0); the W fragments of the next
+    // two 16-deep k-blocks per iteration (kp % 32 == 0; lane half h holds k =
+    // kb + 8h .. kb + 8h + 7 of k-block kb); the W fragments of the next
     // iteration are loaded during this one's MFMAs (register double buffer)
     float4 wv[TPW][4], wn[TPW][4];
     auto load_w = [&](int s, float4 (&dst)[TPW][4]) {
@@ -293,7 +309,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
         for (int i = 0; i < TPW; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int kk = h * kh + s + 4 * j;
+                const int kk = s + 16 * (j >> 1) + 8 * h + 4 * (j & 1);
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (tile_on[i] && row_ok[i]) {
                     const float* wr = wrow[i] + kk;
@@ -419,7 +435,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
                     o.y = ok ? tf(v[u].y, c + 1, sc4.y, sh4.y) : 0.f;
                     o.z = ok ? tf(v[u].z, c + 2, sc4.z, sh4.z) : 0.f;
                     o.w = ok ? tf(v[u].w, c + 3, sc4.w, sh4.w) : 0.f;
-                    *reinterpret_cast<float4*>(As + r * lda + c) = o;
+                    put_a(r, c, o);
                 }
             }
         } else
@@ -456,7 +472,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
                     o.y = (ok && c + 1 < k) ? pro_apply(pro, gr, c + 1, v[u].y) : 0.f;
                     o.z = (ok && c + 2 < k) ? pro_apply(pro, gr, c + 2, v[u].z) : 0.f;
                     o.w = (ok && c + 3 < k) ? pro_apply(pro, gr, c + 3, v[u].w) : 0.f;
-                    *reinterpret_cast<float4*>(As + r * lda + c) = o;
+                    put_a(r, c, o);
                 }
             }
         }
@@ -467,26 +483,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     f32x16 acc[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) acc[i] = f32x16{};
-    const float* ap = As + c32 * lda + h * kh;
+    const uint16_t* ap = Ap + c32 * kp;
+    const int asw = c32 & am;
     if constexpr (TPW != 1) load_w(0, wn);
-    for (int s = 0; s < kh; s += 16) {
+    for (int s = 0; s < kp; s += 32) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) wv[i][j] = wn[i][j];
-        if (s + 16 < kh) load_w(s + 16, wn);
-        float4 av[4];
+        if (s + 32 < kp) load_w(s + 32, wn);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) av[j] = *reinterpret_cast<const float4*>(ap + s + 4 * j);
+        for (int b = 0; b < 2; ++b) {
+            const int ao = (((s + 16 * b) >> 3) + h) ^ asw;
+            Pieces pa;
+            pa.hi = *reinterpret_cast<const s16x8*>(ap + 8 * ao);
+            pa.mid = *reinterpret_cast<const s16x8*>(ap + aplane + 8 * ao);
+            pa.lo = *reinterpret_cast<const s16x8*>(ap + 2 * aplane + 8 * ao);
 #pragma unroll
-        for (int i = 0; i < TPW; ++i) {
-            if (!tile_on[i]) continue;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[i] = mfma(av[j].x, wv[i][j].x, acc[i]);
-                acc[i] = mfma(av[j].y, wv[i][j].y, acc[i]);
-                acc[i] = mfma(av[j].z, wv[i][j].z, acc[i]);
-                acc[i] = mfma(av[j].w, wv[i][j].w, acc[i]);
+            for (int i = 0; i < TPW; ++i) {
+                if (!tile_on[i]) continue;
+                const float4 u = wv[i][2 * b], v = wv[i][2 * b + 1];
+                const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                acc[i] = mfma3(pa, split8(x), acc[i]);
             }
         }
     }
@@ -498,7 +516,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     // row sums by 8 threads per row (DPP butterfly), one sqrt and one division
     // per row, then a multiply per element — instead of a 32-lane shuffle
     // reduction per row and a division per element
-    if (l2 && !a.z_out && !a.stats_out && n * (FM + 1) <= FM * lda) {
+    if (l2 && !a.z_out && !a.stats_out && n * (FM + 1) <= aw) {
         __syncthreads();  // every wave is done reading As
         float* zsq = As;  // [n][FM + 1]
 #pragma unroll
@@ -1428,7 +1446,7 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     const int kp = mlp::pad8(a.k);
     const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
-    const size_t lds = (2 * kp + mlp::FM * (kp + 4) + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
+    const size_t lds = (2 * kp + 3 * mlp::FM * kp / 2 + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
     if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
     return RT_OK;
 }
@@ -1450,7 +1468,7 @@ extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_arg
         blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
     }
     // LDS carve-up of the kernel built for tpw tiles at the larger k of the two
-    const size_t lds = (2 * kp_max + mlp::FM * (kp_max + 4) + 4 * tpw * mlp::FM) * sizeof(float) +
+    const size_t lds = (2 * kp_max + 3 * mlp::FM * kp_max / 2 + 4 * tpw * mlp::FM) * sizeof(float) +
                        mlp::FM * sizeof(int64_t) + 16;
     if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
     mlp::FwdLaunch L{};

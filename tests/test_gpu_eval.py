@@ -48,22 +48,35 @@ def test_generate_recommendations_vs_reference(device, golden):
     np.testing.assert_allclose(ue, g["user_emb"], rtol=1e-5, atol=1e-6)
     np.testing.assert_allclose(ie, g["item_emb"], rtol=1e-5, atol=1e-6)
     full = g["user_emb"][g["test_users"]].astype(np.float64) @ g["item_emb"].astype(np.float64).T
-    n_exact = 0
+    n_exact = n_near = 0
     for r, u in enumerate(users):
         got, want = np.array(recs[u]), g["recs"][r]
         assert len(got) == len(want) == 100
         assert not (set(got.tolist()) & set(train[u]))
+        # smallest gap between consecutive reference scores over the list and the
+        # first item past it (excluded items out): the scores are ~0.3, where one
+        # fp32 ulp is 3e-8, so a list whose gaps all exceed 1e-7 cannot reorder
+        # under last-bit differences of the embeddings and must match exactly
+        s = full[r].copy()
+        s[[x for x in train[u]]] = -np.inf
+        gap = (-np.diff(np.sort(s)[::-1][:101])).min()
+        n_near += gap <= 3e-8
         if np.array_equal(got, want):
             n_exact += 1
             continue
+        assert gap <= 1e-7, (r, gap)
         # tie-aware: positions may differ only inside groups of (near-)equal scores
         sg, sw = full[r, got], full[r, want]
         np.testing.assert_allclose(sg, sw, rtol=0, atol=1e-5)
         kth = sw[-1]
         assert set(got[sg > kth + 1e-5].tolist()) == set(want[sw > kth + 1e-5].tolist()), r
-    print(f"generate_recommendations: {n_exact}/{len(users)} lists identical to the reference's")
-    # observed 298/300 (the other two differ only inside exact-score ties)
-    assert n_exact >= 298, n_exact
+    print(f"generate_recommendations: {n_exact}/{len(users)} lists identical to the reference's "
+          f"({n_near} lists hold two scores within one fp32 ulp)")
+    # the reference data has no exact score ties; 4 of its 300 lists hold a pair
+    # of scores within 3e-8 (one ulp). Observed 298/300 identical with the fp32
+    # MFMA towers (round 3) and 297/300 with the split-bf16 towers (round 4):
+    # every other list identical
+    assert n_exact >= len(users) - n_near, (n_exact, n_near)
 
 
 def test_generate_recommendations_pad_excluded_vs_reference(device, golden):
