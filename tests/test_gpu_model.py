@@ -303,3 +303,31 @@ def test_cpu_tensors_raise():
     t = UserTower(10, 32, [64, 32])
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         t(torch.randn(4, 10))
+
+
+def test_tower_forward_is_fp32_class(dev):
+    """The tower kernels take fp32 products on the bf16 MFMA (three-piece split,
+    DESIGN.md §5 note i). Against a float64 evaluation of the same module, the
+    device output must be as accurate as torch's own fp32 CPU forward (k = 256
+    and 128 reductions, eval BatchNorm, ReLU, final L2 normalise)."""
+    import copy
+    UserTower, _, _, _ = _mods()
+    torch.manual_seed(7)
+    t = UserTower(256, 128, [256, 128], dropout_rate=0.0)
+    for mod in t.mlp:
+        if isinstance(mod, nn.BatchNorm1d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+    t.eval()
+    x = torch.randn(4096, 256)
+    ref_mlp = copy.deepcopy(t.mlp).double()
+    with torch.no_grad():
+        z64 = ref_mlp(x.double())
+        ref = z64 / z64.norm(dim=1, keepdim=True)
+        z32 = copy.deepcopy(t.mlp)(x)
+        cpu32 = z32 / z32.norm(dim=1, keepdim=True)
+        got = t.to(dev)(x.to(dev)).cpu().double()
+    err_dev = (got - ref).abs().max().item()
+    err_cpu = (cpu32.double() - ref).abs().max().item()
+    assert err_dev <= 4 * err_cpu + 1e-7, (err_dev, err_cpu)
+    assert err_dev < 2e-6, err_dev
