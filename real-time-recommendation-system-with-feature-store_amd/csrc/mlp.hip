@@ -99,7 +99,7 @@ struct PhaseProbe {
 #define RT_WT_STORES 1
 #endif
 __device__ __forceinline__ void st_act(float* p, float v) {
-#if defined(RT_WT_STORES) && !defined(RT_WT_DWORD_PLAIN)
+#ifdef RT_WT_STORES
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
     *p = v;
@@ -226,13 +226,6 @@ constexpr int FM = 32;  // rows per block
 
 __host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // k padded to whole 32-deep iterations
 
-// epilogue scratch (RT_EPI_T4): one 32x32 accumulator tile per wave and tile,
-// rows padded to 36 floats (16-B aligned row reads)
-constexpr int kEpiLd = 36, kEpiTile = 32 * kEpiLd;
-__host__ __device__ constexpr int epi_floats(int region, int tiles_per_wave) {
-    return region > 4 * tiles_per_wave * kEpiTile ? region : 4 * tiles_per_wave * kEpiTile;
-}
-
 template <int TPW, bool KVEC>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 2))) void linear_fwd_kernel(FwdLaunch L) {
     const bool g1 = blockIdx.x >= L.split;
@@ -241,7 +234,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     constexpr int NT = 4 * TPW;  // column tiles in the block
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int k = a.k, n = a.n;
-    const int kp = pad8(k), aplane = FM * kp, aw = epi_floats(3 * aplane / 2, TPW);
+    const int kp = pad8(k), aplane = FM * kp, aw = 3 * aplane / 2;
     // 16-B chunk c of row r sits at chunk c ^ (r & am): the 32 rows of a
     // ds_read_b128 then cover the 64 banks without padding (with a 16-B pad
     // per row the k = 256 tile took 54 KB and 2 blocks per CU instead of 3)
@@ -571,13 +564,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     }
     double* const stats = a.stats_out ? a.stats_out + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
                                                        bid % RT_STAT_SLOTS) * 2 * n : nullptr;
-    const bool full = row0 + FM <= m && a.z_out && !l2 && act_is_piecewise_linear(a.act);  // block-uniform
-#ifdef RT_EPI_T4
-    const bool t4 = full && (n % 32) == 0;
-    if (t4) __syncthreads();  // every wave is done reading the A planes (the scratch below)
-#else
-    constexpr bool t4 = false;
-#endif
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
         const int ct = w + 4 * i;
@@ -585,28 +571,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
         const bool col_ok = col < n;
         const float b = (col_ok && a.bias) ? a.bias[col] : 0.f;
         float s1 = 0.f, s2 = 0.f;
-        if (t4) {
-            // full row block, z leaving as 16-B write-through stores: the tile
-            // goes through a wave-private LDS scratch (a 4-B sc1 store is one
-            // fabric write, ~6x the 16-B store's time per byte)
-            if (ct * 32 >= n) continue;  // wave-uniform
-            float* scr = As + (w * TPW + i) * kEpiTile;
-            const float sl = act_slope(a.act);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float z = acc[i][r] + b;
-                scr[((r & 3) + 8 * (r >> 2) + 4 * h) * kEpiLd + c32] = z;
-                const float av = act_pwl(sl, z);
-                s1 += av;
-                s2 += av * av;
-            }
-            wave_lds_sync();
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int rr = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
-                st_act4(a.z_out + (row0 + rr) * n + ct * 32 + c4, *reinterpret_cast<const float4*>(scr + rr * kEpiLd + c4));
-            }
-        } else if (full) {
+        if (row0 + FM <= m && a.z_out && !l2 && act_is_piecewise_linear(a.act)) {
             // full row block (the C2 hidden layers): no per-element predicates,
             // 32-bit offsets from one base pointer
             if (ct * 32 >= n) continue;  // wave-uniform
@@ -1042,46 +1007,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     double* const gps = want_stats ? a.g_prev_stats + (static_cast<int64_t>(my_seg) * RT_STAT_SLOTS +
                                                         bid % RT_STAT_SLOTS) * 2 * k : nullptr;
     const float psl = act_slope(a.prev_act);
-#ifdef RT_EPI_T4
-    // g_prev leaves as 16-B write-through stores through a wave-private LDS
-    // scratch (over the dz tile and its pieces, free once every wave is past
-    // the reduction)
-    const bool t4 = fast && (k % 32) == 0;
-    if (t4) __syncthreads();
-#else
-    constexpr bool t4 = false;
-#endif
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
         const int kk = (w + 4 * i) * 32 + c32;
         const bool col_ok = kk < k;
         float s1 = 0.f, s2 = 0.f;
         if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform: tile past k
-        if (t4) {
-            const int64_t rb = row0 + 4 * h;
-            float* scr = sm + (w * TPWK + i) * kEpiTile;
-            const float* zv = zpre[i];
-            const float pm = pmean[i], pi = pinv[i];
-            const bool drop = a.prev_drop_p > 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int lr = (r & 3) + 8 * (r >> 2);
-                float gv = acc[i][r];
-                if (drop) gv = dropout_keep(pseed, rb + lr, kk, a.prev_drop_p) ? gv * pscale : 0.f;
-                scr[(lr + 4 * h) * kEpiLd + c32] = gv;
-                const float xh = (act_pwl(psl, zv[r]) - pm) * pi;
-                s1 += gv;
-                s2 += gv * xh;
-            }
-            if (!want_stats) s1 = s2 = 0.f;
-            wave_lds_sync();
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int rr = (lane >> 3) + 8 * j, c4 = (lane & 7) * 4;
-                st_act4(a.g_prev + (row0 + rr) * k + (w + 4 * i) * 32 + c4,
-                        *reinterpret_cast<const float4*>(scr + rr * kEpiLd + c4));
-            }
-        } else if (fast) {
+        if (fast) {
             const int64_t rb = row0 + 4 * h;
             float* gp = a.g_prev + rb * k + kk;
             const float* zv = zpre[i];
@@ -1514,7 +1446,7 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     const int kp = mlp::pad8(a.k);
     const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
-    const size_t lds = (2 * kp + mlp::epi_floats(3 * mlp::FM * kp / 2, tpw) + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
+    const size_t lds = (2 * kp + 3 * mlp::FM * kp / 2 + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
     if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
     return RT_OK;
 }
@@ -1536,7 +1468,7 @@ extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_arg
         blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
     }
     // LDS carve-up of the kernel built for tpw tiles at the larger k of the two
-    const size_t lds = (2 * kp_max + mlp::epi_floats(3 * mlp::FM * kp_max / 2, tpw) + 4 * tpw * mlp::FM) * sizeof(float) +
+    const size_t lds = (2 * kp_max + 3 * mlp::FM * kp_max / 2 + 4 * tpw * mlp::FM) * sizeof(float) +
                        mlp::FM * sizeof(int64_t) + 16;
     if (lds > 160 * 1024) return RT_ERR_UNSUPPORTED;
     mlp::FwdLaunch L{};
@@ -1619,10 +1551,6 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
                          3 * static_cast<size_t>(mlp::FM) * (np + 8) * sizeof(uint16_t) + 16;
         lds = l > lds ? l : lds;
         blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
-    }
-    {   // the epilogue scratch (RT_EPI_T4) reuses the dz region: 4 waves x tpwk tiles
-        const size_t le = static_cast<size_t>(mlp::epi_floats(0, tpwk)) * sizeof(float) + 16;
-        lds = lds > le ? lds : le;
     }
     if (all_dz_fusable(args, n_args)) return RT_OK;  // dz computed by the dW launch
     mlp::BwdLaunch L{};
