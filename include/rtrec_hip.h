@@ -217,6 +217,10 @@ typedef struct {
     float* wt_out;           /* optional [k, n]: the launch also writes Wᵀ (row kk = column kk
                                 of w), which the backward's dz launch reads as rt_linear_bwd_args.wt
                                 (NULL = skip) */
+    float* a_out;            /* optional [m, k] (k % 4 == 0, 16-B aligned): the launch also writes
+                                the transformed input rows it stages (after the previous block's
+                                act / BN / dropout prologue and the gather), which the backward's
+                                dW launch reads as rt_linear_bwd_args.a_in (NULL = skip) */
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
@@ -279,6 +283,9 @@ typedef struct {
                                 dz inside its dW launch: the dz launch of the pair is then a no-op
                                 and dz_ws is NOT written; dbias, dgamma, dbeta come from the dW
                                 launch (ignored when the layer does not qualify) */
+    const float* a_in;       /* optional [m, k] = rt_linear_fwd_args.a_out of this step: the dW
+                                launch reads A from it as is instead of recomputing it from src /
+                                ids / prev_* (those still serve the dz launch); NULL = recompute */
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);

@@ -245,8 +245,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     uint16_t* const Ap = reinterpret_cast<uint16_t*>(As);
     float* rowpart = As + aw;            // [NT][FM]
     int64_t* srow = reinterpret_cast<int64_t*>(rowpart + NT * FM);  // [FM]
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
+    const int64_t row0 = static_cast<int64_t>(bid) * FM;
+    const int64_t m = a.m;
     // the transformed A values go to LDS as their three bf16 pieces (split3)
     auto put_a = [&](int r, int c, float4 o) {
+        // the staged (transformed) row also to a_out for this Linear's dW launch
+        if (a.a_out && c < k && row0 + r < m) st_act4(a.a_out + (row0 + r) * k + c, o);
         uint32_t h0, m0, l0, h1, m1, l1;
         split3(o.x, o.y, h0, m0, l0);
         split3(o.z, o.w, h1, m1, l1);
@@ -255,10 +261,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
         *reinterpret_cast<uint2*>(q + aplane) = make_uint2(m0, m1);
         *reinterpret_cast<uint2*>(q + 2 * aplane) = make_uint2(l0, l1);
     };
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, c32 = lane & 31;
-    const int64_t row0 = static_cast<int64_t>(bid) * FM;
-    const int64_t m = a.m;
     RT_PP_DECL
     if (blockIdx.x == 0 && a.zero_buf)
         for (int64_t e = tid; e < a.zero_words; e += 256) a.zero_buf[e] = 0.0;
@@ -1143,7 +1145,10 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
     if (r_begin >= m) return;  // a padding split (block-uniform, before any barrier)
     RT_PP_DECL
-    const bool gather = PRO == 0 && a.ids != nullptr;  // (the host refuses ids with a transformed input)
+    // A rows: the forward's staged copy (a_in, read as is: PRO 0) or recomputed from src
+    const bool gather = PRO == 0 && a.ids != nullptr && !a.a_in;  // (the host refuses ids with a transformed input)
+    const float* const asrc = a.a_in ? a.a_in : a.src;
+    const int64_t ald = a.a_in ? static_cast<int64_t>(k) : static_cast<int64_t>(a.ld_src);
     const bool two = a.seg_split > 0;
 
     // staging columns of this thread (the same for every staged row)
@@ -1152,7 +1157,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     // BN affine of the previous block for this thread's 4 A columns, per row segment
     float4 sc0 = make_float4(1.f, 1.f, 1.f, 1.f), sc1 = sc0;
     float4 sh0 = make_float4(0.f, 0.f, 0.f, 0.f), sh1 = sh0;
-    if (a.prev_mode == 1 || a.prev_mode == 2) {
+    if ((a.prev_mode == 1 || a.prev_mode == 2) && !a.a_in) {
         // one load per (segment, column) for the whole block, through LDS: with
         // every thread loading its own 4 columns x 2 segments x 4 arrays, the
         // 512 threads x ~750 blocks of a C2 launch hammered the same few L2
@@ -1272,7 +1277,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
             if (e < DW_R * VK && r < r_end) {
                 const int64_t sr = gather ? srow[r - r_begin] : r;
                 if (sr >= 0) {
-                    const float* ap = a.src + sr * a.ld_src + gk;
+                    const float* ap = asrc + sr * ald + gk;
                     if constexpr (VEC) {
                         if (gk < k) v = *reinterpret_cast<const float4*>(ap);
                     } else {
@@ -1444,6 +1449,7 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
         return RT_ERR_INVALID;
     if (a.prev_mode == 1 && (!a.prev_stats || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
+    if (a.a_out && ((a.k % 4) != 0 || (reinterpret_cast<uintptr_t>(a.a_out) & 15) != 0)) return RT_ERR_INVALID;
     const int kp = mlp::pad8(a.k);
     const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
     const size_t lds = (2 * kp + 3 * mlp::FM * kp / 2 + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
@@ -1453,6 +1459,11 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
 
 extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_args, void* stream) {
     if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+#ifdef RT_NO_AIN  // A/B build: no staged-input copy (the dW launch recomputes A)
+    rt_linear_fwd_args noa[2];
+    for (int g = 0; g < n_args; ++g) { noa[g] = args[g]; noa[g].a_out = nullptr; }
+    args = noa;
+#endif
     int tpw = 1, kp_max = 0;
     bool kvec = true;
     unsigned blocks[2] = {0u, 0u};
@@ -1618,6 +1629,11 @@ static void dw_plan(const rt_linear_bwd_args* args, int n_args, bool small_k, un
 
 extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream) {
     if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+#ifdef RT_NO_AIN
+    rt_linear_bwd_args noa[2];
+    for (int g = 0; g < n_args; ++g) { noa[g] = args[g]; noa[g].a_in = nullptr; }
+    args = noa;
+#endif
     mlp::BwdLaunch L{};
     unsigned blocks[2] = {0u, 0u};
     int pro = -1;
@@ -1640,7 +1656,7 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
         (g ? L.tk1 : L.tk0) = tks[g] ? tks[g] : 1u;
         (g ? L.rps1 : L.rps0) = rps;
         int p = 0;
-        if (a.prev_mode != 0) p = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
+        if (a.prev_mode != 0 && !a.a_in) p = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
         // one kernel for both: prologue 3 ⊇ 2 ⊇ 1 (dropout p = 0 keeps everything);
         // a raw input (0) and a transformed one cannot share a kernel
         if (pro >= 0 && (pro == 0) != (p == 0)) {
@@ -1648,8 +1664,10 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
             return r0 ? r0 : rt_linear_bwd_dw_f32_multi(&args[1], 1, stream);
         }
         pro = p > pro ? p : pro;
-        (g ? L.vec1 : L.vec0) = (a.n % 4) == 0 && (a.k % 4) == 0 && (a.ld_src % 4) == 0 &&
-                                (reinterpret_cast<uintptr_t>(a.src) & 15) == 0 &&
+        const float* asrc = a.a_in ? a.a_in : a.src;
+        const int ald = a.a_in ? a.k : a.ld_src;
+        (g ? L.vec1 : L.vec0) = (a.n % 4) == 0 && (a.k % 4) == 0 && (ald % 4) == 0 &&
+                                (reinterpret_cast<uintptr_t>(asrc) & 15) == 0 &&
                                 (reinterpret_cast<uintptr_t>(a.dz_ws) & 15) == 0;
     }
     L.a0 = args[0];

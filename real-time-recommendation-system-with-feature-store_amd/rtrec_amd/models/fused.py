@@ -202,6 +202,7 @@ class ChainCtx:
     normalize: bool = True
     seg_split: int = 0  # > 0: rows [0, seg_split) and [seg_split, m) are separate BN batches
     wts: List[Optional[torch.Tensor]] = field(default_factory=list)  # Wᵀ of each Linear (fwd writes, dz reads)
+    ains: List[Optional[torch.Tensor]] = field(default_factory=list)  # transformed inputs (fwd writes, dW reads)
 
 
 def _stream(t: torch.Tensor):
@@ -354,6 +355,14 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         if wt is not None:
             a.wt_out = wt.data_ptr()
         ctx.wts.append(wt)
+        # training: the launch also writes the transformed input it stages (act →
+        # BN → dropout of the previous block), which this Linear's dW launch then
+        # reads as is instead of recomputing it (rt_linear_fwd_args.a_out / a_in)
+        ain = None
+        if li > 0 and lin.training and lin.in_features % 4 == 0:
+            ain = torch.empty((m, lin.in_features), dtype=torch.float32, device=dev)
+            a.a_out = ain.data_ptr()
+        ctx.ains.append(ain)
         if li < L:
             z = torch.empty((m, lin.out_features), dtype=torch.float32, device=dev)
             a.z_out = z.data_ptr()
@@ -523,5 +532,7 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
             a.g_prev = g.data_ptr()
             if li < len(ctx.wts) and ctx.wts[li] is not None:
                 a.wt = ctx.wts[li].data_ptr()
+            if li < len(ctx.ains) and ctx.ains[li] is not None:
+                a.a_in = ctx.ains[li].data_ptr()
         layers.append(a)
     return layers, dsrc, keep

@@ -50,7 +50,7 @@ class LinearFwdArgs(ctypes.Structure):
         ("bn_eps", c_f32), ("bn_momentum", c_f32), ("drop_p", c_f32), ("drop_seed", c_u64),
         ("seed_offset", vp), ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
         ("num_batches_tracked", vp), ("seg_split", c_i64), ("zero_buf", vp), ("zero_words", c_i64),
-        ("wt_out", vp),
+        ("wt_out", vp), ("a_out", vp),
     ]
 
 
@@ -64,7 +64,7 @@ class LinearBwdArgs(ctypes.Structure):
         ("prev_mode", c_int), ("prev_act", c_int), ("prev_mean", vp), ("prev_invstd", vp),
         ("prev_gamma", vp), ("prev_beta", vp), ("prev_drop_p", c_f32), ("prev_drop_seed", c_u64),
         ("seed_offset", vp), ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp), ("seg_split", c_i64),
-        ("dbias_slots", vp), ("wt", vp), ("fuse_dz", c_int),
+        ("dbias_slots", vp), ("wt", vp), ("fuse_dz", c_int), ("a_in", vp),
     ]
 
 
