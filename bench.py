@@ -376,8 +376,8 @@ def c1_epoch(dev):
 # the csrc files each PMC-profiled kernel family is built from (its traffic
 # figure is reused only while these are unchanged; tools/traffic_json.py)
 KERNEL_SOURCES = {
-    "linear_fwd": ["mlp.hip", "rt_common.h"], "linear_bwd_dz": ["mlp.hip", "rt_common.h"],
-    "linear_bwd_dw": ["mlp.hip", "rt_common.h"], "loss_fwd_bwd": ["loss.hip", "rt_common.h"],
+    "linear_fwd": ["mlp.hip", "split3.h", "rt_common.h"], "linear_bwd_dz": ["mlp.hip", "split3.h", "rt_common.h"],
+    "linear_bwd_dw": ["mlp.hip", "split3.h", "rt_common.h"], "loss_fwd_bwd": ["loss.hip", "split3.h", "rt_common.h"],
     "clip_adam": ["optim.hip", "rt_common.h"],
     "flatip_topk_c4": ["topk_api.hip", "topk_f16.hip", "topk_impl.h", "topk_v1.h", "topk_v2.h", "topk_v3.h",
                        "topk_v4.h", "topk_dense.h", "rt_sort.h", "rt_common.h"],

@@ -1,4 +1,5 @@
-// Two-tower losses, fused forward + backward (fp32 scores on v_mfma_f32_32x32x2_f32).
+// Two-tower losses, fused forward + backward (fp32 scores and gradients as
+// three-piece bf16 MFMA sextets, split3.h).
 //
 // Replaces (src/models/two_tower.py):
 //   compute_similarity      :380-404   → rt_similarity_f32
@@ -20,11 +21,13 @@
 //   the streamed rows follows the accumulator layout), so dU = dS·P (row pass)
 //   and dP = dSᵀ·U (column pass) need no LDS transpose; dS = w/B·(softmax − I).
 //   The 4 waves' partials are summed through LDS, one atomic per element per span.
-// The k-order inside an S chain is permuted (k = h·D/2 + s) so that every
-// fragment is a contiguous 16-byte vector.
+// Every MFMA operand is an fp32 value taken as its three bf16 pieces; the
+// k-order of an S chain is that of the 32x32x16 MFMA (lane half h holds
+// k = 16kb + 8h .. +7 of k-block kb), so every fragment is two contiguous float4.
 #include <float.h>
 
 #include "rt_common.h"
+#include "split3.h"
 
 namespace rt {
 size_t ib16_workspace_bytes(int64_t b, int64_t nx, int d);
@@ -38,9 +41,6 @@ constexpr int kMaxD = 256;
 constexpr int kMaxNeg = 64;
 constexpr int NG = 16;  // negatives reduced together
 
-__device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
 
 __device__ __forceinline__ int tile_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -102,33 +102,41 @@ __device__ __forceinline__ void store_rows(float* __restrict__ S, const float4 (
         *reinterpret_cast<float4*>(S + row * (DP + LDP) + c) = v[u];
     }
 }
-// fixed-row fragments: lane (c, h) holds F[f0 + c][h·DP/2 + s], s < DP/2
+// fixed-row pieces per 16-deep k-block (fp32 products on the bf16 MFMA,
+// split3.h): lane (c, h) holds the split of F[f0 + c][16kb + 8h .. 16kb + 8h + 7]
+using fsplit::Pieces;
+using fsplit::split8;
+using fsplit::mfma3;
 template <int DP, typename T>
-__device__ __forceinline__ void load_fixed(const T* __restrict__ F, int64_t f0, int64_t n, int D,
-                                           float (&fx)[DP / 2]) {
+__device__ __forceinline__ void load_fixed3(const T* __restrict__ F, int64_t f0, int64_t n, int D,
+                                            Pieces (&pf)[DP / 16]) {
     const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
     const int64_t r = f0 + c;
 #pragma unroll
-    for (int q = 0; q < DP / 8; ++q) {
-        const int k = h * (DP / 2) + 4 * q;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (r < n && k < D) v = load4<T>(F + r * D + k);
-        fx[4 * q] = v.x; fx[4 * q + 1] = v.y; fx[4 * q + 2] = v.z; fx[4 * q + 3] = v.w;
+    for (int kb = 0; kb < DP / 16; ++kb) {
+        const int k = 16 * kb + 8 * h;  // D % 8 == 0: a k-block half is all in or all out
+        float4 u = make_float4(0.f, 0.f, 0.f, 0.f), v = u;
+        if (r < n && k < D) {
+            u = load4<T>(F + r * D + k);
+            v = load4<T>(F + r * D + k + 4);
+        }
+        const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        pf[kb] = split8(x);
     }
 }
-// acc[r] = <streamed row tile_row(r,h) of Ss, fixed row (lane & 31)> (raw dots)
+// acc[r] = <streamed row tile_row(r,h) of Ss, fixed row (lane & 31)> (raw dots),
+// one bf16 MFMA sextet per 16-deep k-block
 template <int DP>
-__device__ __forceinline__ f32x16 s_tile(const float* __restrict__ Ss, const float (&fx)[DP / 2]) {
+__device__ __forceinline__ f32x16 s_tile3(const float* __restrict__ Ss, const Pieces (&pf)[DP / 16]) {
     const int lane = threadIdx.x & 63, c = lane & 31, h = lane >> 5;
-    const float* ap = Ss + c * (DP + LDP) + h * (DP / 2);
+    const float* ap = Ss + c * (DP + LDP) + 8 * h;
     f32x16 acc = {};
 #pragma unroll
-    for (int q = 0; q < DP / 8; ++q) {
-        const float4 av = *reinterpret_cast<const float4*>(ap + 4 * q);
-        acc = mfma(av.x, fx[4 * q], acc);
-        acc = mfma(av.y, fx[4 * q + 1], acc);
-        acc = mfma(av.z, fx[4 * q + 2], acc);
-        acc = mfma(av.w, fx[4 * q + 3], acc);
+    for (int kb = 0; kb < DP / 16; ++kb) {
+        const float4 u = *reinterpret_cast<const float4*>(ap + 16 * kb);
+        const float4 v = *reinterpret_cast<const float4*>(ap + 16 * kb + 4);
+        const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        acc = mfma3(split8(x), pf[kb], acc);
     }
     return acc;
 }
@@ -159,8 +167,8 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
     if (js < a.ib_blocks) {
         // ---- in-batch partial lse: S^T tiles (items j × users i) ----
         float* Ss = sm_f + w * 32 * (DP + LDP);
-        float fx[DP / 2];
-        load_fixed<DP, T>(U, i0, a.b, D, fx);
+        Pieces pf[DP / 16];
+        load_fixed3<DP, T>(U, i0, a.b, D, pf);
         const int64_t t0 = static_cast<int64_t>(js) * SPAN + 32 * w, t1 = t0 + 128;
         float4 buf[DP / 8];
         load_rows<DP, T>(P, t0, a.nx, D, buf);
@@ -172,7 +180,7 @@ __global__ __launch_bounds__(256) void loss_fwd_kernel(Args a) {
             store_rows<DP>(Ss, buf);
             wave_lds_sync();
             if (q == 0 && t1 < a.nx) load_rows<DP, T>(P, t1, a.nx, D, buf);  // prefetch
-            const f32x16 acc = s_tile<DP>(Ss, fx);
+            const f32x16 acc = s_tile3<DP>(Ss, pf);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 if (tt + tile_row(r, h) < a.nx) {
@@ -378,8 +386,8 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
     if (!a.grad || !ib || f0 >= n_fixed || s0 >= n_str) return;
 
     float* Ss = sm_b + w * 32 * (DP + LDP);
-    float fx[DP / 2];
-    load_fixed<DP, T>(Fm, f0, n_fixed, D, fx);
+    Pieces pf[DP / 16];
+    load_fixed3<DP, T>(Fm, f0, n_fixed, D, pf);
     const int64_t t0 = s0 + 32 * w, t1 = t0 + 128;
     float4 buf[DP / 8];
     load_rows<DP, T>(Sm, t0, n_str, D, buf);
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
         wave_lds_sync();
         if (q == 0 && t1 < n_str) load_rows<DP, T>(Sm, t1, n_str, D, buf);  // prefetch
         // st[r]: streamed row tile_row(r,h) x fixed col c
-        const f32x16 st = s_tile<DP>(Ss, fx);
+        const f32x16 st = s_tile3<DP>(Ss, pf);
         float ds[16];
         const int64_t fcol = f0 + c;
 #pragma unroll
@@ -410,12 +418,25 @@ __global__ __launch_bounds__(256) void loss_bwd_kernel(Args a, float wb_eff, boo
             }
             ds[r] = v;
         }
-        // dF[fixed c][d] += Σ_r dS[fixed c][streamed tile_row(r,h)] · Str[tile_row(r,h)][d]
+        // dF[fixed c][d] += Σ_r dS[fixed c][streamed tile_row(r,h)] · Str[tile_row(r,h)][d]:
+        // k-block b of the sextets = accumulator registers 8b..8b+7 of both lane
+        // halves (streamed rows 16b..16b+15), so dS enters as it lies (lane-local)
+        Pieces pds[2];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const float x[8] = {ds[8 * b], ds[8 * b + 1], ds[8 * b + 2], ds[8 * b + 3],
+                                ds[8 * b + 4], ds[8 * b + 5], ds[8 * b + 6], ds[8 * b + 7]};
+            pds[b] = split8(x);
+        }
 #pragma unroll
         for (int dt = 0; dt < DT; ++dt) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r)
-                acc[dt] = mfma(ds[r], Ss[tile_row(r, h) * (DP + LDP) + dt * 32 + c], acc[dt]);
+            for (int b = 0; b < 2; ++b) {
+                float y[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] = Ss[tile_row(8 * b + j, h) * (DP + LDP) + dt * 32 + c];
+                acc[dt] = mfma3(pds[b], split8(y), acc[dt]);
+            }
         }
         wave_lds_sync();
     }
