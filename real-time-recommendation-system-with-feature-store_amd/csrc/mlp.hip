@@ -1565,7 +1565,10 @@ extern "C" int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream
 static void dw_plan(const rt_linear_bwd_args* args, int n_args, bool small_k, unsigned* tn, unsigned* tk,
                     int64_t* splits, int64_t& rps) {
     const int bn = small_k ? 128 : 64, bk = small_k ? 32 : 64;
-    const int64_t cap = small_k ? 128 : 64;
+#ifndef RT_DW_CAP_SMALLK
+#define RT_DW_CAP_SMALLK 128
+#endif
+    const int64_t cap = small_k ? RT_DW_CAP_SMALLK : 64;
     int64_t work = 0, rmin = mlp::DW_R;
     for (int g = 0; g < n_args; ++g) {
         const rt_linear_bwd_args& a = args[g];
