@@ -272,10 +272,13 @@ typedef struct {
     float* dsrc;             /* [m, k] input grad (first layer), or NULL */
     int64_t seg_split;       /* as in rt_linear_fwd_args: g_stats, save_mean/invstd,
                                 prev_mean/invstd and g_prev_stats are then [2][...] */
-    double* dbias_slots;     /* optional fp64 [RT_STAT_SLOTS][n], caller-zeroed: the dz launch
+    double* dbias_slots;     /* optional fp64 [RT_STAT_SLOTS + 1][n], caller-zeroed: the dz launch
                                 adds each row block's column sums of dz (slot = block % SLOTS)
                                 and the dW launch folds the slots into dbias — bounded
-                                same-address contention; NULL = the dW launch sums dz itself */
+                                same-address contention; NULL = the dW launch sums dz itself.
+                                With fuse_dz the dW launch adds its splits' sums into the slots
+                                and the last block of each n-tile folds them; row RT_STAT_SLOTS
+                                then holds that launch's per-tile ticket counters (uint64) */
     const float* wt;         /* optional [k, n] = Wᵀ of THIS step's w (rt_linear_fwd_args.wt_out):
                                 dA = dz·W then reads contiguous rows of it (NULL = columns of w) */
     int fuse_dz;             /* 1: a layer with no dA (g_prev and dsrc NULL), grad_mode 1-3, a

@@ -1185,6 +1185,11 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         }
     }
     const bool do_bias = a.dbias != nullptr && (DZF || a.dbias_slots == nullptr) && by == 0;
+    // fused dz with slots: same-address fp32 dbias atomics from every split of a
+    // tile cost ~10 us per C2 step (a timing build without them); instead the
+    // splits add into the fp64 slots and the tile's last-arriving block folds
+    // them (ticket counter in slot row RT_STAT_SLOTS, zeroed with the slots)
+    const bool slot_bias = DZF && do_bias && a.dbias_slots != nullptr;
 
     if (gather) {
         for (int64_t t = tid; t < r_end - r_begin; t += DW_NT) {
@@ -1358,10 +1363,21 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
             sb.x += v.x; sb.y += v.y; sb.z += v.z; sb.w += v.w;
         }
         const int cb = n0 + tid * 4;
-        if (cb < n) atomicAdd(&a.dbias[cb], sb.x);
-        if (cb + 1 < n) atomicAdd(&a.dbias[cb + 1], sb.y);
-        if (cb + 2 < n) atomicAdd(&a.dbias[cb + 2], sb.z);
-        if (cb + 3 < n) atomicAdd(&a.dbias[cb + 3], sb.w);
+        if (slot_bias) {
+            // fused-dz launch: the split's column sums go to fp64 slot bz % SLOTS
+            // (contention splits / SLOTS per address instead of splits); the
+            // tile's last block folds the slots below
+            double* sl = a.dbias_slots + static_cast<int64_t>(bz % RT_STAT_SLOTS) * n;
+            if (cb < n) atomicAdd(&sl[cb], static_cast<double>(sb.x));
+            if (cb + 1 < n) atomicAdd(&sl[cb + 1], static_cast<double>(sb.y));
+            if (cb + 2 < n) atomicAdd(&sl[cb + 2], static_cast<double>(sb.z));
+            if (cb + 3 < n) atomicAdd(&sl[cb + 3], static_cast<double>(sb.w));
+        } else {
+            if (cb < n) atomicAdd(&a.dbias[cb], sb.x);
+            if (cb + 1 < n) atomicAdd(&a.dbias[cb + 1], sb.y);
+            if (cb + 2 < n) atomicAdd(&a.dbias[cb + 2], sb.z);
+            if (cb + 3 < n) atomicAdd(&a.dbias[cb + 3], sb.w);
+        }
     }
     // acc[t][r] = dW[n0 + ncol-tile + (r&3) + 8(r>>2) + 4h][k0 + kcol0 + 32t]
     auto add_row = [&](int t, int r, int kk) {
@@ -1376,6 +1392,31 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
 #pragma unroll
         for (int r = 0; r < 16; ++r)
             if ((r >> 3) == grp) add_row(t, r, kk);
+    }
+    if (slot_bias) {  // block-uniform
+        __shared__ int last_s;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slot atomics are performed
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            unsigned long long* cnt = reinterpret_cast<unsigned long long*>(a.dbias_slots + static_cast<int64_t>(RT_STAT_SLOTS) * n);
+            const unsigned long long nsplit = static_cast<unsigned long long>((m + rows_per_split - 1) / rows_per_split);
+            last_s = atomicAdd(&cnt[bx], 1ull) == nsplit - 1 ? 1 : 0;
+        }
+        __syncthreads();
+        if (last_s) {
+            // every split of this tile has added: fold the slots in slot order
+            // (returning adds of 0 read them at the memory side, where they live)
+            for (int cl = tid; cl < BN; cl += DW_NT) {
+                const int c = n0 + cl;
+                if (c >= n) continue;
+                double v = 0.0;
+#pragma unroll
+                for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) v += atomicAdd(&a.dbias_slots[static_cast<int64_t>(sl) * n + c], 0.0);
+                atomicAdd(&a.dbias[c], static_cast<float>(v));
+            }
+        }
     }
     RT_PP_END(3)
 }
