@@ -289,6 +289,17 @@ typedef struct {
     const float* a_in;       /* optional [m, k] = rt_linear_fwd_args.a_out of this step: the dW
                                 launch reads A from it as is instead of recomputing it from src /
                                 ids / prev_* (those still serve the dz launch); NULL = recompute */
+    float* dw_part;          /* optional [splits][n][k] fp32 (splits: rt_linear_bwd_dw_splits):
+                                the dW launch STORES each row split's tile sum here instead of
+                                adding it into dw with atomics; a later launch folds it (fold_*) */
+    const float* fold_src;   /* optional side task of this args' dz launch (fold_in 0) or dW launch
+                                (fold_in 1): fold_dst[e] += sum over s < fold_splits of
+                                fold_src[s * fold_words + e], in s order, e < fold_words — the
+                                fold of an EARLIER launch's dw_part (fold_words % 4 == 0) */
+    float* fold_dst;
+    int64_t fold_words;
+    int fold_splits;
+    int fold_in;
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);
@@ -296,6 +307,10 @@ int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);
  * their dW launch computes dz itself (rt_linear_bwd_args.fuse_dz), else 0 —
  * the caller may then skip the dz call. Host-only, no GPU work. */
 int rt_linear_bwd_dz_fused(const rt_linear_bwd_args* args, int n_args);
+/* Row splits per argument set that rt_linear_bwd_dw_f32_multi(args, n_args) will
+ * use (the planner is joint over the n_args sets): the first dimension of
+ * their dw_part buffers. Host-only, no GPU work. */
+int rt_linear_bwd_dw_splits(const rt_linear_bwd_args* args, int n_args, int64_t* splits);
 /* the two launches of rt_linear_bwd_f32, separately (same arguments, same
  * order on one stream): dz/dgamma/dbeta/dA, then dW/dbias from dz_ws. */
 int rt_linear_bwd_dz_f32(const rt_linear_bwd_args* args, void* stream);

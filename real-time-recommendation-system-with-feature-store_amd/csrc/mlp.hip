@@ -40,7 +40,46 @@ struct BwdLaunch {
     int64_t rps0, rps1;     // dW: rows per split
     unsigned tn0, tk0, tn1, tk1;  // dW: tile grid of each group
     bool vec0, vec1;              // dW: float4 staging loads
+    int ngroups;                  // argument sets in this launch (a1 is a copy of a0 when 1)
 };
+
+// Side task of a dz (which = 0) or dW (which = 1) launch: fold an EARLIER dW
+// launch's row-split partial tiles (rt_linear_bwd_args.dw_part → fold_*) into
+// its gradient. Work item = (4 words, a group of kFoldG splits); its loads are
+// all issued before the adds; one float4 of fp32 atomics per item when the
+// splits form several groups (a plain read-add-store when one). Every thread
+// of the launch takes items, before the launch's own work.
+constexpr int kFoldG = 8;
+__device__ __forceinline__ void fold_side(const BwdLaunch& L, int which) {
+    const int64_t nt = static_cast<int64_t>(gridDim.x) * blockDim.x;
+    const int64_t gt = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (int g = 0; g < L.ngroups; ++g) {
+        const rt_linear_bwd_args& f = g ? L.a1 : L.a0;
+        if (!f.fold_src || f.fold_in != which || f.fold_splits <= 0) continue;
+        const int64_t n4 = f.fold_words / 4;
+        const int ng = (f.fold_splits + kFoldG - 1) / kFoldG;
+        for (int64_t it = gt; it < n4 * ng; it += nt) {
+            const int64_t e = it % n4;
+            const int s0 = static_cast<int>(it / n4) * kFoldG;
+            float4 v[kFoldG];
+#pragma unroll
+            for (int j = 0; j < kFoldG; ++j)
+                v[j] = s0 + j < f.fold_splits
+                           ? reinterpret_cast<const float4*>(f.fold_src + static_cast<int64_t>(s0 + j) * f.fold_words)[e]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            float4 t = v[0];
+#pragma unroll
+            for (int j = 1; j < kFoldG; ++j) { t.x += v[j].x; t.y += v[j].y; t.z += v[j].z; t.w += v[j].w; }
+            float* d = f.fold_dst + 4 * e;
+            if (ng == 1) {
+                const float4 o = *reinterpret_cast<const float4*>(d);
+                *reinterpret_cast<float4*>(d) = make_float4(o.x + t.x, o.y + t.y, o.z + t.z, o.w + t.w);
+            } else {
+                atomicAdd(d, t.x); atomicAdd(d + 1, t.y); atomicAdd(d + 2, t.z); atomicAdd(d + 3, t.w);
+            }
+        }
+    }
+}
 
 
 // ---------------------------------------------------------------------------
@@ -607,6 +646,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 // some CUs; the register cap moves the accumulators from AGPRs to VGPRs, no spill)
 template <int TPWK>  // 32-col dA tiles per wave (k <= 128*TPWK)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void linear_bwd_dz_kernel(BwdLaunch L) {
+    fold_side(L, 0);
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
@@ -1087,6 +1127,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     __shared__ __attribute__((aligned(16))) float aff_s[2][2][BK];  // [segment][scale, shift][tile column]
     __shared__ __attribute__((aligned(16))) float dzc_s[DZF ? 2 : 1][5][DZF ? BN : 4];  // DZF: [seg][A,B,C,M,I][col]
 
+    fold_side(L, 1);
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args a = g1 ? L.a1 : L.a0;  // by value: fields loaded once
     const int64_t rows_per_split = g1 ? L.rps1 : L.rps0;
@@ -1383,7 +1424,16 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     auto add_row = [&](int t, int r, int kk) {
         const int nn = n0 + (w % NTN) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const float v = acc[t][r] + red[((w * T + t) * 16 + r) * 64 + lane];
-        if (nn < n) atomicAdd(&a.dw[static_cast<int64_t>(nn) * k + kk], v);
+        if (nn < n) {
+            if (a.dw_part) {  // folded by a later launch; write-through (1 us/step better than plain)
+#ifdef RT_DW_PART_PLAIN
+                a.dw_part[(static_cast<int64_t>(bz) * n + nn) * k + kk] = v;
+#else
+                st_act(a.dw_part + (static_cast<int64_t>(bz) * n + nn) * k + kk, v);
+#endif
+            }
+            else atomicAdd(&a.dw[static_cast<int64_t>(nn) * k + kk], v);
+        }
     };
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -1540,6 +1590,9 @@ static int validate_bwd(const rt_linear_bwd_args* args) {
     if ((a.prev_mode == 1 || a.prev_mode == 2) &&
         (!a.prev_mean || !a.prev_invstd || !a.prev_gamma || !a.prev_beta))
         return RT_ERR_INVALID;
+    if (a.fold_src && (!a.fold_dst || a.fold_words % 4 != 0 || a.fold_splits <= 0 || a.fold_in < 0 || a.fold_in > 1 ||
+                       (reinterpret_cast<uintptr_t>(a.fold_src) & 15) || (reinterpret_cast<uintptr_t>(a.fold_dst) & 15)))
+        return RT_ERR_INVALID;
     return RT_OK;
 }
 
@@ -1561,10 +1614,15 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
         lds = l > lds ? l : lds;
         blocks[g] = static_cast<unsigned>((a.m + mlp::FM - 1) / mlp::FM);
     }
-    if (all_dz_fusable(args, n_args)) return RT_OK;  // dz computed by the dW launch
+    if (all_dz_fusable(args, n_args)) {  // dz computed by the dW launch
+        for (int g = 0; g < n_args; ++g)
+            if (args[g].fold_src && args[g].fold_in == 0) return RT_ERR_INVALID;  // its fold would never run
+        return RT_OK;
+    }
     mlp::BwdLaunch L{};
     L.a0 = args[0];
     L.a1 = n_args > 1 ? args[1] : args[0];
+    L.ngroups = n_args;
     L.split = blocks[0];
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
     if (total == 0) return RT_OK;
@@ -1673,6 +1731,7 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     }
     L.a0 = args[0];
     L.a1 = n_args > 1 ? args[1] : args[0];
+    L.ngroups = n_args;
     if (n_args == 1) { L.tn1 = L.tn0; L.tk1 = L.tk0; L.rps1 = L.rps0; L.vec1 = L.vec0; }
     L.split = blocks[0];
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
@@ -1700,6 +1759,24 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     }
 #undef RT_DW
     return check_launch("linear_bwd_dw_kernel");
+}
+
+extern "C" int rt_linear_bwd_dw_splits(const rt_linear_bwd_args* args, int n_args, int64_t* splits) {
+    if (!args || !splits || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+#ifdef RT_NO_DW_PART  // A/B build: callers keep the atomic dW adds
+    return RT_ERR_UNSUPPORTED;
+#endif
+    bool small_k = true;
+    for (int g = 0; g < n_args; ++g) {
+        const int v = validate_bwd(&args[g]);
+        if (v) return v;
+        small_k = small_k && args[g].k <= 32;
+    }
+    unsigned tns[2] = {1u, 1u}, tks[2] = {1u, 1u};
+    int64_t nsplit[2] = {0, 0}, rps = mlp::DW_R;
+    dw_plan(args, n_args, small_k, tns, tks, nsplit, rps);
+    for (int g = 0; g < n_args; ++g) splits[g] = nsplit[g];
+    return RT_OK;
 }
 
 extern "C" int rt_linear_bwd_dw_f32(const rt_linear_bwd_args* args, void* stream) {

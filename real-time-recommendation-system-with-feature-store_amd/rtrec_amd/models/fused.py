@@ -396,8 +396,10 @@ def chain_backward(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
     into the slab. Returns d src (dense input) when ``want_dsrc``."""
     layers, dsrc, keep = _backward_plan(blocks, ctx, dout, slab, want_dsrc, seed_offset, stats_arena, attach)
     st = _stream(dout)
-    for a in layers:  # per Linear: dz (+dA) then dW (+dbias), timed separately (bench roofline)
-        _launch_bwd([a], st)
+    groups = [[a] for a in layers]
+    keep += _plan_partials(groups, dout.device)
+    for g in groups:  # per Linear: dz (+dA) then dW (+dbias), timed separately (bench roofline)
+        _launch_bwd(g, st)
     return dsrc
 
 
@@ -410,11 +412,45 @@ def chain_backward_pair(first: tuple, second: tuple) -> None:
     l2, _, keep2 = _backward_plan(*second)
     st = _stream(first[2])
     if len(l1) == len(l2):
-        for a, b in zip(l1, l2):
-            _launch_bwd([a, b], st)
+        groups = [[a, b] for a, b in zip(l1, l2)]
+        keep1 += _plan_partials(groups, first[2].device)
     else:
-        for a in l1 + l2:
-            _launch_bwd([a], st)
+        groups = [[a] for a in l1 + l2]
+    for g in groups:
+        _launch_bwd(g, st)
+
+
+def _plan_partials(groups: list, dev) -> list:
+    """Launch groups in execution order: every dW launch but the last STORES its
+    row-split tile sums (rt_linear_bwd_args.dw_part) instead of adding them
+    with fp32 atomics, and the next group's first launch (its dz, or its dW
+    when that layer's dz is fused) folds them into the gradient (fold_*): the
+    atomics were bound by their bytes (≈ 11 MB per C2 step at ≈ 1.3 TB/s).
+    Returns the partial buffers (kept alive by the caller)."""
+    lib = native.lib()
+    if not hasattr(lib, "rt_linear_bwd_dw_splits"):
+        return []
+    keep = []
+    for gi in range(len(groups) - 1):
+        grp, nxt = groups[gi], groups[gi + 1]
+        if len(grp) != len(nxt):
+            continue
+        arr = (LinearBwdArgs * len(grp))(*grp)
+        splits = (ctypes.c_int64 * len(grp))()
+        if lib.rt_linear_bwd_dw_splits(arr, len(grp), splits) != 0:
+            continue
+        narr = (LinearBwdArgs * len(nxt))(*nxt)
+        fold_in = 1 if lib.rt_linear_bwd_dz_fused(narr, len(nxt)) else 0
+        for a, b, sp in zip(grp, nxt, splits):
+            words = a.n * a.k
+            if sp < 1 or words % 4 or b.fold_src:
+                continue
+            part = torch.empty(sp * words, dtype=torch.float32, device=dev)
+            keep.append(part)
+            a.dw_part = part.data_ptr()
+            b.fold_src, b.fold_dst, b.fold_words = part.data_ptr(), a.dw, words
+            b.fold_splits, b.fold_in = sp, fold_in
+    return keep
 
 
 def _launch_bwd(group: list, st) -> None:

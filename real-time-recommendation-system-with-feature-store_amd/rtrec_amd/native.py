@@ -64,7 +64,8 @@ class LinearBwdArgs(ctypes.Structure):
         ("prev_mode", c_int), ("prev_act", c_int), ("prev_mean", vp), ("prev_invstd", vp),
         ("prev_gamma", vp), ("prev_beta", vp), ("prev_drop_p", c_f32), ("prev_drop_seed", c_u64),
         ("seed_offset", vp), ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp), ("seg_split", c_i64),
-        ("dbias_slots", vp), ("wt", vp), ("fuse_dz", c_int), ("a_in", vp),
+        ("dbias_slots", vp), ("wt", vp), ("fuse_dz", c_int), ("a_in", vp), ("dw_part", vp),
+        ("fold_src", vp), ("fold_dst", vp), ("fold_words", c_i64), ("fold_splits", c_int), ("fold_in", c_int),
     ]
 
 
@@ -86,6 +87,7 @@ SIGNATURES = {
     "rt_linear_bwd_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_bwd_dz_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_bwd_dz_fused": (c_int, [ctypes.POINTER(LinearBwdArgs), c_int]),
+    "rt_linear_bwd_dw_splits": (c_int, [ctypes.POINTER(LinearBwdArgs), c_int, ctypes.POINTER(c_i64)]),
     "rt_linear_bwd_dw_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_fwd_f32_multi": (c_int, [ctypes.POINTER(LinearFwdArgs), c_int, vp]),
     "rt_linear_bwd_dz_f32_multi": (c_int, [ctypes.POINTER(LinearBwdArgs), c_int, vp]),
