@@ -375,6 +375,10 @@ def c1_epoch(dev):
 
 # the csrc files each PMC-profiled kernel family is built from (its traffic
 # figure is reused only while these are unchanged; tools/traffic_json.py)
+# kernels whose fp32 products run on the bf16 MFMA through the three-piece split
+SPLIT_BF16_KERNELS = ("linear_fwd", "linear_bwd_dz", "loss_fwd_bwd")
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md
+
 KERNEL_SOURCES = {
     "linear_fwd": ["mlp.hip", "split3.h", "rt_common.h"], "linear_bwd_dz": ["mlp.hip", "split3.h", "rt_common.h"],
     "linear_bwd_dw": ["mlp.hip", "split3.h", "rt_common.h"], "loss_fwd_bwd": ["loss.hip", "split3.h", "rt_common.h"],
@@ -660,6 +664,10 @@ def main():
     roof["traffic"] = tb
     roof["traffic_unit"] = "bytes/launch (PMC)"
     roof["traffic_source"] = tsrc
+    if dominant in SPLIT_BF16_KERNELS:
+        roof["peak_note"] = ("fp32-class products as 6 bf16 MFMAs each (three-piece split, DESIGN.md §5 note i): "
+                             f"the instruction ceiling of this kernel is {PEAK_BF16_TFLOPS / 6:.0f} TFLOP/s "
+                             f"(frac {achieved / (PEAK_BF16_TFLOPS / 6):.3f} of it); peak above = the fp32 MFMA")
     roof.update({"kernel": dominant, "launches_per_step": d["count"] / args.steps,
                  "measured": ("HIP events around each launch over an eager replay of the timed steps "
                               "(a GPU spin ahead of each launch keeps host submission out of the interval)"
