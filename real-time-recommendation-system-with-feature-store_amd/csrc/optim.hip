@@ -50,34 +50,44 @@ __global__ __launch_bounds__(256) void clip_adam_kernel(float* __restrict__ p, f
                                                         const int32_t* step_dev, double* __restrict__ zbuf,
                                                         int64_t zwords) {
     __shared__ float coef_s, step_size_s, bc2_sqrt_s;
-    if (threadIdx.x == 0) {
+    // this thread's first element is loaded before the clip factor is known
+    // (it does not depend on it): the two memory round trips overlap
+    const int64_t e0 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    float p0 = 0.f, g0 = 0.f, m0 = 0.f, v0 = 0.f;
+    if (e0 < n) { p0 = p[e0]; g0 = g[e0]; m0 = m[e0]; v0 = v[e0]; }
+    if (threadIdx.x < 64) {
+        // wave 0 sums the per-tensor norms in parallel (a fixed tree: deterministic)
         double tot = 0.0;
-        for (int t = 0; t < n_tensors; ++t) tot += sumsq[t];
-        const float total = static_cast<float>(sqrt(tot));
-        const float coef = max_norm / (total + 1e-6f);
-        coef_s = coef < 1.f ? coef : 1.f;
-        const int st = step_dev ? *step_dev : step;
-        const float lr_v = lr_dev ? *lr_dev : lr;
-        const double bc1 = 1.0 - pow(static_cast<double>(b1), st);
-        const double bc2 = 1.0 - pow(static_cast<double>(b2), st);
-        step_size_s = static_cast<float>(lr_v / bc1);
-        bc2_sqrt_s = static_cast<float>(sqrt(bc2));
+        for (int t = threadIdx.x; t < n_tensors; t += 64) tot += sumsq[t];
+        tot = wave_sum(tot);
+        if (threadIdx.x == 0) {
+            const float total = static_cast<float>(sqrt(tot));
+            const float coef = max_norm / (total + 1e-6f);
+            coef_s = coef < 1.f ? coef : 1.f;
+            const int st = step_dev ? *step_dev : step;
+            const float lr_v = lr_dev ? *lr_dev : lr;
+            const double bc1 = 1.0 - pow(static_cast<double>(b1), st);
+            const double bc2 = 1.0 - pow(static_cast<double>(b2), st);
+            step_size_s = static_cast<float>(lr_v / bc1);
+            bc2_sqrt_s = static_cast<float>(sqrt(bc2));
+        }
     }
     __syncthreads();
     const float coef = coef_s, step_size = step_size_s, bc2s = bc2_sqrt_s;
     const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
-    for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < n; e += stride) {
-        const float pv = p[e];
-        float gv = g[e] * coef;
+    auto update = [&](int64_t e, float pv, float graw, float mo, float vo) {
+        float gv = graw * coef;
         if (wd != 0.f) gv = gv + wd * pv;
-        const float mv = m[e] + (1.f - b1) * (gv - m[e]);          // exp_avg.lerp_(grad, 1-beta1)
-        const float vv = v[e] * b2 + (1.f - b2) * gv * gv;         // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
+        const float mv = mo + (1.f - b1) * (gv - mo);              // exp_avg.lerp_(grad, 1-beta1)
+        const float vv = vo * b2 + (1.f - b2) * gv * gv;           // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2)
         const float denom = sqrtf(vv) / bc2s + eps;
         m[e] = mv;
         v[e] = vv;
         p[e] = pv - step_size * (mv / denom);
         g[e] = 0.f;  // consumed: the next step accumulates from zero
-    }
+    };
+    if (e0 < n) update(e0, p0, g0, m0, v0);
+    for (int64_t e = e0 + stride; e < n; e += stride) update(e, p[e], g[e], m[e], v[e]);
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; e < zwords; e += stride) zbuf[e] = 0.0;
 }
 
