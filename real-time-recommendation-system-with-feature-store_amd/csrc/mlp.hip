@@ -646,7 +646,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 // some CUs; the register cap moves the accumulators from AGPRs to VGPRs, no spill)
 template <int TPWK>  // 32-col dA tiles per wave (k <= 128*TPWK)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void linear_bwd_dz_kernel(BwdLaunch L) {
+#ifdef RT_FOLD_FIRST
     fold_side(L, 0);
+#endif
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
@@ -937,6 +939,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
         }
     }
     if (!a.g_prev && !a.dsrc) {
+#ifndef RT_FOLD_FIRST
+        fold_side(L, 0);
+#endif
         RT_PP_END(2)
         return;
     }
@@ -1059,6 +1064,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             }
         }
     }
+#ifndef RT_FOLD_FIRST
+    fold_side(L, 0);
+#endif
     RT_PP_END(2)
 }
 
@@ -1127,7 +1135,9 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     __shared__ __attribute__((aligned(16))) float aff_s[2][2][BK];  // [segment][scale, shift][tile column]
     __shared__ __attribute__((aligned(16))) float dzc_s[DZF ? 2 : 1][5][DZF ? BN : 4];  // DZF: [seg][A,B,C,M,I][col]
 
+#ifdef RT_FOLD_FIRST
     fold_side(L, 1);
+#endif
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_bwd_args a = g1 ? L.a1 : L.a0;  // by value: fields loaded once
     const int64_t rows_per_split = g1 ? L.rps1 : L.rps0;
@@ -1141,7 +1151,12 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
     const int n0 = static_cast<int>(bx) * BN, k0 = static_cast<int>(by) * BK;
     const int64_t r_begin = static_cast<int64_t>(bz) * rows_per_split;
     const int64_t r_end = (r_begin + rows_per_split) < m ? (r_begin + rows_per_split) : m;
-    if (r_begin >= m) return;  // a padding split (block-uniform, before any barrier)
+    if (r_begin >= m) {  // a padding split (block-uniform, before any barrier)
+#ifndef RT_FOLD_FIRST
+        fold_side(L, 1);
+#endif
+        return;
+    }
     RT_PP_DECL
     // A rows: the forward's staged copy (a_in, read as is: PRO 0) or recomputed from src
     const bool gather = PRO == 0 && a.ids != nullptr && !a.a_in;  // (the host refuses ids with a transformed input)
@@ -1468,6 +1483,9 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
             }
         }
     }
+#ifndef RT_FOLD_FIRST
+    fold_side(L, 1);
+#endif
     RT_PP_END(3)
 }
 
