@@ -172,6 +172,9 @@ int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* pos_items, in
 #ifndef RT_STAT_SLOTS
 #define RT_STAT_SLOTS 8
 #endif
+#if RT_STAT_SLOTS > 15
+#error "RT_STAT_SLOTS > 15: the host arenas (rtrec_amd/models/fused.py STAT_SLOTS) hold 16 slot rows, one of them for ticket counters"
+#endif
 
 typedef struct {
     const float* src;        /* [src_rows, ld_src] input rows (features or prev z) */
@@ -221,6 +224,22 @@ typedef struct {
                                 the transformed input rows it stages (after the previous block's
                                 act / BN / dropout prologue and the gather), which the backward's
                                 dW launch reads as rt_linear_bwd_args.a_in (NULL = skip) */
+    /* BatchNorm finalised by its producer (optional; with stats_out, a training BN after this
+     * Linear): the launch's last block per argument set — found by a ticket counter at word
+     * nseg·RT_STAT_SLOTS·2n of stats_out (past the slots; caller-zeroed with them) — turns the
+     * column sums into the batch mean / invstd and the running-stat updates ONCE, instead of
+     * every block of the consuming launch re-deriving them from the fp64 slots. The consuming
+     * launch then passes prev_final = 1 and reads them from its save_mean / save_invstd. */
+    float* fin_save_mean;    /* [nseg][n] batch means (the consumer's save_mean); NULL = no finalisation */
+    float* fin_save_invstd;  /* [nseg][n] 1/sqrt(biased var + eps) */
+    float* fin_running_mean; /* [n] momentum update, segment 0 then segment 1 (NULL = skip) */
+    float* fin_running_var;  /* [n] with the unbiased batch variance */
+    int64_t* fin_num_batches_tracked; /* += nseg (NULL = skip) */
+    float fin_eps;
+    float fin_momentum;
+    int prev_final;          /* prev_mode 1 only: 1 = the producing launch finalised the batch
+                                statistics (save_mean / save_invstd hold them; prev_stats, the
+                                running stats and num_batches_tracked are not touched here) */
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);

@@ -210,6 +210,63 @@ __device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, f
     shift = __builtin_fmaf(-mean, scale, beta);
 }
 
+// BatchNorm finalisation by the producing forward launch (rt_linear_fwd_args
+// fin_*): every block calls this after its stats atomics; the group's last
+// block (ticket counter past the slots) derives the batch mean / invstd of
+// each segment from the fp64 slot sums — read by returning atomic adds of 0,
+// at the memory side where the slots live — and applies the running-stat
+// updates in segment order, with the same arithmetic as the consumer-side
+// finalisation below (linear_fwd_kernel, prev_final = 0).
+__device__ __noinline__ void bn_finalize_last(const rt_linear_fwd_args& a, unsigned nblk) {
+    __shared__ int last_s;
+    const int tid = threadIdx.x, n = a.n;
+    const bool two = a.seg_split > 0;
+    const int nseg = two ? 2 : 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slot atomics are performed
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned long long* cnt =
+            reinterpret_cast<unsigned long long*>(a.stats_out + static_cast<int64_t>(nseg) * RT_STAT_SLOTS * 2 * n);
+        last_s = atomicAdd(cnt, 1ull) == static_cast<unsigned long long>(nblk) - 1ull ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last_s) return;
+    for (int c = tid; c < n; c += blockDim.x) {
+        for (int sg = 0; sg < nseg; ++sg) {
+            const int64_t ms = two ? (sg == 0 ? a.seg_split : a.m - a.seg_split) : a.m;
+            double* ps = a.stats_out + static_cast<int64_t>(sg) * RT_STAT_SLOTS * 2 * n;
+            double v1[RT_STAT_SLOTS], v2[RT_STAT_SLOTS];
+#pragma unroll
+            for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                v1[sl] = atomicAdd(&ps[static_cast<int64_t>(sl) * 2 * n + c], 0.0);
+                v2[sl] = atomicAdd(&ps[static_cast<int64_t>(sl) * 2 * n + n + c], 0.0);
+            }
+            double s1 = 0.0, s2 = 0.0;  // slot order
+#pragma unroll
+            for (int sl = 0; sl < RT_STAT_SLOTS; ++sl) {
+                s1 += v1[sl];
+                s2 += v2[sl];
+            }
+            const double md = s1 / static_cast<double>(ms);
+            double vd = s2 / static_cast<double>(ms) - md * md;
+            vd = vd > 0.0 ? vd : 0.0;
+            const float mean = static_cast<float>(md);
+            const float invstd = static_cast<float>(1.0 / sqrt(vd + static_cast<double>(a.fin_eps)));
+            const float var_f = static_cast<float>(ms > 1 ? vd * static_cast<double>(ms) / static_cast<double>(ms - 1) : vd);
+            a.fin_save_mean[sg * n + c] = mean;
+            if (a.fin_save_invstd) a.fin_save_invstd[sg * n + c] = invstd;
+            if (a.fin_running_mean) {
+                const float mo = a.fin_momentum;
+                a.fin_running_mean[c] = (1.f - mo) * a.fin_running_mean[c] + mo * mean;
+                a.fin_running_var[c] = (1.f - mo) * a.fin_running_var[c] + mo * var_f;
+            }
+        }
+    }
+    if (tid == 0 && a.fin_num_batches_tracked) *a.fin_num_batches_tracked += nseg;
+}
+
 // ---------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------
@@ -339,10 +396,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 
     // BatchNorm of the previous block: this block's batch is its row segment;
     // block 0 derives every segment (it owns the save/running-stat writes,
-    // applied in segment order like two sequential tower calls)
+    // applied in segment order like two sequential tower calls) — unless the
+    // producing launch finalised the batch statistics already (prev_final):
+    // then every block reads its segment's mean / invstd (4 floats a column)
     const bool two = a.seg_split > 0;
     const int my_seg = (two && row0 >= a.seg_split) ? 1 : 0;
-    if (a.prev_mode == 1 || a.prev_mode == 2) {
+    if (a.prev_mode == 1 && a.prev_final) {
+        for (int c = tid; c < k; c += 256)
+            bn_affine(a.bn_gamma[c], a.bn_beta[c], a.save_mean[my_seg * k + c], a.save_invstd[my_seg * k + c], scale[c],
+                      shift[c]);
+    } else if (a.prev_mode == 1 || a.prev_mode == 2) {
         const int nseg = two ? 2 : 1;
         for (int c = tid; c < k; c += 256) {
             for (int sg = 0; sg < nseg; ++sg) {
@@ -614,6 +677,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
             }
         }
     }
+    if (stats && a.fin_save_mean) bn_finalize_last(a, g1 ? gridDim.x - L.split : L.split);
     if (l2) {
         __syncthreads();
         const int nt_used = (n + 31) / 32;
@@ -1516,6 +1580,9 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
     if (a.prev_mode == 1 && (!a.prev_stats || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.prev_mode == 2 && (!a.running_mean || !a.running_var || !a.bn_gamma || !a.bn_beta)) return RT_ERR_INVALID;
     if (a.a_out && ((a.k % 4) != 0 || (reinterpret_cast<uintptr_t>(a.a_out) & 15) != 0)) return RT_ERR_INVALID;
+    if (a.fin_save_mean && (!a.stats_out || !a.fin_save_invstd || (!a.fin_running_mean != !a.fin_running_var)))
+        return RT_ERR_INVALID;
+    if (a.prev_final && (a.prev_mode != 1 || !a.save_mean || !a.save_invstd)) return RT_ERR_INVALID;
     const int kp = mlp::pad8(a.k);
     const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
     const size_t lds = (2 * kp + 3 * mlp::FM * kp / 2 + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
@@ -1704,23 +1771,28 @@ static void dw_plan(const rt_linear_bwd_args* args, int n_args, bool small_k, un
     for (int g = 0; g < n_args; ++g) splits[g] = args[g].m > 0 ? (args[g].m + rps - 1) / rps : 0;
 }
 
-extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream) {
-    if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
-#ifdef RT_NO_AIN
-    rt_linear_bwd_args noa[2];
-    for (int g = 0; g < n_args; ++g) { noa[g] = args[g]; noa[g].a_in = nullptr; }
-    args = noa;
-#endif
+// the dW prologue a set needs: 0 raw input (or the forward's staged rows,
+// a_in), 1 BN(act) of a piecewise-linear act, 2 + dropout, 3 any activation
+static int dw_prologue(const rt_linear_bwd_args& a) {
+    if (a.prev_mode == 0 || a.a_in) return 0;
+    return !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
+}
+// two sets whose prologues cannot share a kernel (a raw input and a
+// transformed one: prologue 3 ⊇ 2 ⊇ 1, but 0 is disjoint): they run as two
+// single-set launches, each with its own row-split plan
+// (rt_linear_bwd_dw_splits follows the same rule)
+static bool dw_mixed(const rt_linear_bwd_args* args, int n_args) {
+    return n_args == 2 && (dw_prologue(args[0]) == 0) != (dw_prologue(args[1]) == 0);
+}
+
+// one dW launch over n_args sets that share a prologue family; dzf: the dz
+// fusion decided for the whole call (the dz launch decided it jointly too)
+static int dw_launch(const rt_linear_bwd_args* args, int n_args, bool dzf, hipStream_t st) {
     mlp::BwdLaunch L{};
     unsigned blocks[2] = {0u, 0u};
     int pro = -1;
     bool small_k = true;
-    for (int g = 0; g < n_args; ++g) {
-        const int v = validate_bwd(&args[g]);
-        if (v) return v;
-        if (args[g].ids && args[g].prev_mode != 0) return RT_ERR_UNSUPPORTED;  // a gather feeds the first Linear only
-        small_k = small_k && args[g].k <= 32;
-    }
+    for (int g = 0; g < n_args; ++g) small_k = small_k && args[g].k <= 32;
     unsigned tns[2] = {1u, 1u}, tks[2] = {1u, 1u};
     int64_t nsplit[2] = {0, 0}, rps = mlp::DW_R;
     dw_plan(args, n_args, small_k, tns, tks, nsplit, rps);
@@ -1732,14 +1804,8 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
         (g ? L.tn1 : L.tn0) = tns[g] ? tns[g] : 1u;
         (g ? L.tk1 : L.tk0) = tks[g] ? tks[g] : 1u;
         (g ? L.rps1 : L.rps0) = rps;
-        int p = 0;
-        if (a.prev_mode != 0 && !a.a_in) p = !act_is_piecewise_linear(a.prev_act) ? 3 : (a.prev_drop_p > 0.f ? 2 : 1);
-        // one kernel for both: prologue 3 ⊇ 2 ⊇ 1 (dropout p = 0 keeps everything);
-        // a raw input (0) and a transformed one cannot share a kernel
-        if (pro >= 0 && (pro == 0) != (p == 0)) {
-            const int r0 = rt_linear_bwd_dw_f32_multi(&args[0], 1, stream);
-            return r0 ? r0 : rt_linear_bwd_dw_f32_multi(&args[1], 1, stream);
-        }
+        // one kernel for both: prologue 3 ⊇ 2 ⊇ 1 (dropout p = 0 keeps everything)
+        const int p = dw_prologue(a);
         pro = p > pro ? p : pro;
         const float* asrc = a.a_in ? a.a_in : a.src;
         const int ald = a.a_in ? a.k : a.ld_src;
@@ -1755,9 +1821,7 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
     if (total == 0) return RT_OK;
     const dim3 grid(total);
-    hipStream_t st = as_stream(stream);
     const bool vec = L.vec0 && L.vec1;
-    const bool dzf = all_dz_fusable(args, n_args);
 #define RT_DW(BN, BK, P)                                                                                                 \
     do {                                                                                                                 \
         if (dzf) {                                                                                                       \
@@ -1779,6 +1843,28 @@ extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_
     return check_launch("linear_bwd_dw_kernel");
 }
 
+extern "C" int rt_linear_bwd_dw_f32_multi(const rt_linear_bwd_args* args, int n_args, void* stream) {
+    if (!args || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
+#ifdef RT_NO_AIN
+    rt_linear_bwd_args noa[2];
+    for (int g = 0; g < n_args; ++g) { noa[g] = args[g]; noa[g].a_in = nullptr; }
+    args = noa;
+#endif
+    for (int g = 0; g < n_args; ++g) {
+        const int v = validate_bwd(&args[g]);
+        if (v) return v;
+        if (args[g].ids && args[g].prev_mode != 0) return RT_ERR_UNSUPPORTED;  // a gather feeds the first Linear only
+    }
+    hipStream_t st = as_stream(stream);
+    // dz fusion as rt_linear_bwd_dz_f32_multi decided it for the same call: all sets or none
+    const bool dzf = all_dz_fusable(args, n_args);
+    if (dw_mixed(args, n_args)) {
+        const int r0 = dw_launch(&args[0], 1, dzf, st);
+        return r0 ? r0 : dw_launch(&args[1], 1, dzf, st);
+    }
+    return dw_launch(args, n_args, dzf, st);
+}
+
 extern "C" int rt_linear_bwd_dw_splits(const rt_linear_bwd_args* args, int n_args, int64_t* splits) {
     if (!args || !splits || n_args < 1 || n_args > 2) return RT_ERR_INVALID;
 #ifdef RT_NO_DW_PART  // A/B build: callers keep the atomic dW adds
@@ -1792,6 +1878,13 @@ extern "C" int rt_linear_bwd_dw_splits(const rt_linear_bwd_args* args, int n_arg
     }
     unsigned tns[2] = {1u, 1u}, tks[2] = {1u, 1u};
     int64_t nsplit[2] = {0, 0}, rps = mlp::DW_R;
+    if (dw_mixed(args, n_args)) {  // two single-set launches, two plans
+        for (int g = 0; g < 2; ++g) {
+            dw_plan(&args[g], 1, args[g].k <= 32, tns, tks, nsplit, rps);
+            splits[g] = nsplit[0];
+        }
+        return RT_OK;
+    }
     dw_plan(args, n_args, small_k, tns, tks, nsplit, rps);
     for (int g = 0; g < n_args; ++g) splits[g] = nsplit[g];
     return RT_OK;

@@ -102,7 +102,7 @@ struct Plan {
     int v4_joint;        // v4 over > 1 split: one threshold per query from a corpus-wide sample
     size_t fail_bytes;   // v4 joint: per-query flags (union of the split buffers < k)
     int stride, rank;    // v4 sample: every stride-th stage; threshold = rank-th group maximum
-    size_t meta_bytes;   // v4 per-(split, query, half) entry counts
+    size_t meta_bytes;   // v4 per-(split, query) entry counts
     size_t kth_bytes;    // register-list kernel over > 1 split: the shared per-query k-th keys
     int dense;           // 1: fp32 small corpus, GEMM into a score slab + per-query select (topk_dense.h)
 };

@@ -326,7 +326,7 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     red = torch.cat([loss[0:1].to(torch.float64), owned.to(torch.float64).reshape(1).to(loss.device)])
     if world > 1:
         dist.all_reduce(red, op=dist.ReduceOp.SUM, group=group)
-    lv = red[0:1]
+    lv = red[0:1].to(loss.dtype)  # the loss kernel's dtype (the reduction ran in fp64)
     if status is not None:
         _status_update(status, False, n_valid, red[1].round().to(torch.int64))
     if grad_shard is not None:

@@ -186,11 +186,13 @@ def flatl2_topk(q_aug: torch.Tensor, x_aug: torch.Tensor, d: int, k: int,
             bb = exclude_bits.index_select(0, bad).contiguous() if exclude_bits is not None else None
             s2 = torch.empty((nb, k), dtype=torch.float32, device=q_aug.device)
             i2 = torch.empty((nb, k), dtype=torch.int64, device=q_aug.device)
-            f2 = torch.empty(nb, dtype=torch.int32, device=q_aug.device)
-            select_finish(qb, bb, min(512, nx), s2, i2, f2)
+            k2 = min(512, nx)
+            # a re-selection of the whole corpus is exact by construction: no certificate
+            f2 = torch.empty(nb, dtype=torch.int32, device=q_aug.device) if k2 < nx else None
+            select_finish(qb, bb, k2, s2, i2, f2)
             s.index_copy_(0, bad, s2)
             i.index_copy_(0, bad, i2)
-            left = int(f2.sum().item())
+            left = int(f2.sum().item()) if f2 is not None else 0
         elif nb:
             left = nb
         L2_STATS["reselected"] += nb if k_sel < min(512, nx) else 0

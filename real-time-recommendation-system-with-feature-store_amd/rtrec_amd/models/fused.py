@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes
 import itertools
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -213,13 +214,19 @@ def _stream(t: torch.Tensor):
 # this build); the arenas are sized for 16, an upper bound of every library
 # variant's slot count, so a variant build never writes past them
 STAT_SLOTS = 16
+# dbias slots are [RT_STAT_SLOTS + 1][n]: row RT_STAT_SLOTS holds the fused-dz dW
+# launch's per-tile tickets, so a region of STAT_SLOTS + 1 rows covers every variant
+DBIAS_ROWS = STAT_SLOTS + 1
+# BatchNorm batch statistics finalised once by the producing forward launch
+# (rt_linear_fwd_args.fin_*) instead of by every block of the consuming launch
+FINALIZE_BN_IN_PRODUCER = os.environ.get("RTREC_BN_FINAL", "1") != "0"
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
     """fp64 words of BN column sums one forward (or backward) of the chain needs,
-    plus the dbias slots of every Linear ([STAT_SLOTS][n], backward)."""
+    plus the dbias slots of every Linear ([DBIAS_ROWS][n], backward)."""
     return max(1, n_seg * STAT_SLOTS * 2 * sum(b.linear.out_features for b in blocks[:-1])
-               + STAT_SLOTS * sum(b.linear.out_features for b in blocks))
+               + DBIAS_ROWS * sum(b.linear.out_features for b in blocks))
 
 
 def _zero_on_entry(layer, zero_buf: Optional[torch.Tensor]):
@@ -348,10 +355,22 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
                 a.bn_momentum = float(pb.bn.momentum if pb.bn.momentum is not None else 0.1)
                 if pb.bn.training and pb.bn.num_batches_tracked is not None:
                     a.num_batches_tracked = pb.bn.num_batches_tracked.data_ptr()  # +1 in-kernel
+                prod = layers[li - 1]
+                if a.prev_mode == 1 and prod.stats_out and FINALIZE_BN_IN_PRODUCER:
+                    # the producing launch's last block derives mean / invstd and the
+                    # running-stat updates once (rt_linear_fwd_args.fin_*); this launch
+                    # reads them (prev_final)
+                    prod.fin_save_mean, prod.fin_save_invstd = a.save_mean, a.save_invstd
+                    prod.fin_running_mean, prod.fin_running_var = a.running_mean, a.running_var
+                    prod.fin_num_batches_tracked = a.num_batches_tracked
+                    prod.fin_eps, prod.fin_momentum = a.bn_eps, a.bn_momentum
+                    a.prev_final = 1
         a.act = b.act
         # Wᵀ of this Linear for its backward's dA (layers past the first: their
-        # dz launch computes the previous block's gradient)
-        wt = torch.empty((lin.in_features, lin.out_features), dtype=torch.float32, device=dev) if li > 0 else None
+        # dz launch computes the previous block's gradient); training forwards
+        # only — eval / serving forwards have no backward to read it
+        wt = torch.empty((lin.in_features, lin.out_features), dtype=torch.float32, device=dev) \
+            if li > 0 and lin.training else None
         if wt is not None:
             a.wt_out = wt.data_ptr()
         ctx.wts.append(wt)
@@ -494,8 +513,8 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
         off += n_seg * STAT_SLOTS * 2 * wdt
     bslots = []  # dbias slots of Linear li (both BN segments add into the same slots)
     for b in blocks:
-        bslots.append(gst_arena[off:off + STAT_SLOTS * b.linear.out_features])
-        off += STAT_SLOTS * b.linear.out_features
+        bslots.append(gst_arena[off:off + DBIAS_ROWS * b.linear.out_features])
+        off += DBIAS_ROWS * b.linear.out_features
     gs: List[Optional[torch.Tensor]] = [None] * L
     dsrc = torch.empty((m, blocks[0].linear.in_features), dtype=torch.float32, device=dev) if want_dsrc else None
     keep = [dout, gst_arena] + dz_bufs

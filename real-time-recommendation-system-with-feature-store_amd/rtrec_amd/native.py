@@ -51,6 +51,8 @@ class LinearFwdArgs(ctypes.Structure):
         ("seed_offset", vp), ("z_out", vp), ("act", c_int), ("stats_out", vp), ("l2_out", vp), ("norms_out", vp),
         ("num_batches_tracked", vp), ("seg_split", c_i64), ("zero_buf", vp), ("zero_words", c_i64),
         ("wt_out", vp), ("a_out", vp),
+        ("fin_save_mean", vp), ("fin_save_invstd", vp), ("fin_running_mean", vp), ("fin_running_var", vp),
+        ("fin_num_batches_tracked", vp), ("fin_eps", c_f32), ("fin_momentum", c_f32), ("prev_final", c_int),
     ]
 
 

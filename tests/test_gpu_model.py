@@ -171,6 +171,46 @@ def test_fused_train_step_golden(dev, golden):
     np.testing.assert_allclose(losses, g["losses"], rtol=RTOL)
 
 
+def test_fused_train_step_mixed_dw_prologues(dev):
+    """Tower pairs whose paired layers differ in in_features % 4: the user
+    tower's last Linear (in 130) recomputes its input in the dW launch while the
+    item tower's (in 128) reads the forward's staged rows, so the joint dW launch
+    splits into two single-set launches. Their row-split plans must match the
+    partial buffers the caller sized (rt_linear_bwd_dw_splits) and the dz fusion
+    must not add dbias twice. Two steps against oracle.train_step."""
+    from oracle import two_tower as orc
+    from rtrec_amd.models.two_tower import ItemTower, TwoTowerModel, UserTower
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    torch.manual_seed(5)
+    model = TwoTowerModel(UserTower(3, 64, [256, 130], dropout_rate=0.0),
+                          ItemTower(20, 64, [256, 128], dropout_rate=0.0, use_content_embedding=False),
+                          temperature=0.05)
+    us = {k: v.detach().clone() for k, v in model.user_tower.state_dict().items()}
+    its = {k: v.detach().clone() for k, v in model.item_tower.state_dict().items()}
+    biases = {"user_bias": model.user_bias.detach().clone(), "item_bias": model.item_bias.detach().clone()}
+    model.to(dev)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5)
+    g = torch.Generator().manual_seed(9)
+    opt = {}
+    for _ in range(2):
+        u = torch.randn(256, 3, generator=g)
+        p = torch.randn(256, 20, generator=g)
+        n = torch.randn(256, 4, 20, generator=g)
+        r = orc.train_step(us, its, biases, opt, u, p, n, temperature=0.05, lr=1e-3, weight_decay=1e-5)
+        lb = step(u.to(dev), p.to(dev), n.to(dev))
+        np.testing.assert_allclose(float(lb[0].item()), r["loss"], rtol=RTOL)
+    for tname, tower, ref_sd in (("user", model.user_tower, us), ("item", model.item_tower, its)):
+        for k, v in tower.state_dict().items():
+            ref = ref_sd[k].detach().numpy()
+            got = v.detach().cpu().numpy()
+            if "num_batches" in k:
+                assert int(got) == int(ref), k
+                continue
+            diff = np.abs(got - ref)
+            assert np.mean(diff <= 1e-5 + 1e-4 * np.abs(ref)) > 0.995, (tname, k, diff.max())
+            assert diff.max() <= 2.1e-3, (tname, k, diff.max())
+
+
 # ---------------------------------------------------------------------------
 # reference behavioural tests (tests/test_two_tower_model.py) on the GPU path
 # ---------------------------------------------------------------------------

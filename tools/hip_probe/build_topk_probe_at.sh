@@ -1,0 +1,23 @@
+#!/bin/bash
+# Builds tools/hip_probe/topk_probe_<NAME> from the csrc/ and include/ of a git
+# revision (REV=WORKTREE: the working tree), for same-box A/B runs of the
+# top-K kernels (tools/topk_ab.sh). Usage: build_topk_probe_at.sh REV NAME [-DFLAGS...]
+set -e
+REV=$1; NAME=$2; shift 2
+H=$(cd "$(dirname "$0")" && pwd)
+R=$(cd $H/../.. && pwd)
+PKG=real-time-recommendation-system-with-feature-store_amd
+T=$(mktemp -d /tmp/tkp.XXXX)
+mkdir -p $T/csrc $T/include
+if [ "$REV" = WORKTREE ]; then
+  cp $R/$PKG/csrc/* $T/csrc/; cp $R/include/* $T/include/
+else
+  git -C $R archive $REV $PKG/csrc include | tar -x -C $T
+  mv $T/$PKG/csrc/* $T/csrc/
+fi
+C=$T/csrc
+/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -munsafe-fp-atomics -I$T/include -I$C "$@" \
+  $H/topk_probe.hip $C/topk_api.hip $C/topk_f16.hip $C/topk_bf16.hip $C/topk_f32.hip $C/capi.hip \
+  -o $H/topk_probe_$NAME 2>&1 | grep -v "unused\|warning\|note:\|^ *[0-9]* |\|^ *|" || true
+rm -rf $T
+ls -la $H/topk_probe_$NAME

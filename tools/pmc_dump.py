@@ -8,6 +8,9 @@ from collections import defaultdict
 ap = argparse.ArgumentParser()
 ap.add_argument("dbs", nargs="+")
 ap.add_argument("--filter", default="")
+ap.add_argument("--calls", type=int, default=0,
+                help="also print each counter summed over all dispatches / CALLS (per API call: "
+                     "a call may launch a kernel more than once, e.g. the top-K main + rescue pairs)")
 a = ap.parse_args()
 agg = defaultdict(lambda: defaultdict(float))
 cnt = defaultdict(lambda: defaultdict(set))
@@ -24,4 +27,5 @@ for k, d in agg.items():
     print(k)
     for ctr in sorted(d):
         n = len(cnt[k][ctr])
-        print(f"    {ctr:32s} {d[ctr] / n:16.4g}   (dispatches {n})")
+        extra = f"   per call {d[ctr] / a.calls:.4g}" if a.calls else ""
+        print(f"    {ctr:32s} {d[ctr] / n:16.4g}   (dispatches {n}){extra}")
