@@ -507,9 +507,9 @@ def c5_sharded_step(dev, dist, rank, world, reps=10):
     100M-row x 256 bf16 item table row-sharded 12.5M rows (6.4 GB) per GPU
     (weak scaling: the shard and the per-rank batch stay fixed as N grows, the
     table holds 12.5M·N rows), 8,192 users per rank with uniform global positive
-    ids. One step = the sync-free row exchange (id all-gather, every rank
-    gathers the global batch against its own row window, one byte-wise MAX
-    all-reduce of the rows; rtrec_amd/dist/sharded.py::sharded_gather_rows) +
+    ids. One step = the row exchange (ids + row windows all-gather, each owner
+    packs its positions' rows into a fixed segment, one all-gather of the
+    segments; rtrec_amd/dist/sharded.py::sharded_gather_rows) +
     the 16-bit in-batch CE forward+backward of the rank's users against ALL
     gathered rows + the loss all-reduce (sharded_inbatch_step; the table is a
     frozen feature table as in the reference, so no item-gradient exchange). The
@@ -544,11 +544,14 @@ def c5_sharded_step(dev, dist, rank, world, reps=10):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    from rtrec_amd.dist.sharded import LAST_EXCHANGE
     out = {"ms_per_step": 1e3 * el / reps, "n_gpus": world, "table_rows": rows_per * world, "shard_rows": rows_per,
            "emb_dim": dim, "users_per_rank": b, "dtype": "bf16", "loss": float(loss[0].item()),
            "pairs_per_s": world * b * (b * world) * reps / el,
-           "exchange": "id all-gather + window gather + byte-wise MAX all-reduce of rows (+ loss all-reduce); "
-                       "no host sync",
+           "exchange": ("ids + windows all-gather, owner-segment all-gather of rows (one host read of the "
+                        "overflow flag), loss all-reduce" if world > 1 else "none (N = 1: collectives skipped)"),
+           "exchange_mode": LAST_EXCHANGE.get("mode"), "segment_rows": LAST_EXCHANGE.get("segment_rows"),
+           "bytes_exchanged_per_rank": LAST_EXCHANGE.get("bytes_per_rank", 0),
            "scaling": "weak (fixed shard and batch per GPU)"}
     del shard
     torch.cuda.empty_cache()

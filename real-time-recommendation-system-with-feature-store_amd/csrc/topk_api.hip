@@ -208,7 +208,7 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
     if (g_v4_rank >= 0) p.rank = g_v4_rank;
     const int64_t q_pad = static_cast<int64_t>(p.q_tiles) * QT;
     p.cand_bytes = static_cast<size_t>(p.splits) * q_pad * v4::kCap * sizeof(Cand);
-    p.meta_bytes = static_cast<size_t>(p.splits) * q_pad * sizeof(int);
+    p.meta_bytes = static_cast<size_t>(p.splits) * q_pad * 2 * sizeof(int);
     p.fail_bytes = p.v4_joint ? static_cast<size_t>(q_pad) * sizeof(int) : 0;
     p.part_bytes = 0;
     return true;

@@ -21,12 +21,11 @@
 //        the sampled fraction f, with rank / f (the expected appends) at
 //        most RT_TOPK_V4_APPEND_CAP (topk_api.hip::plan_v4_sample).
 //      * main phase: every stage (the sample stages again), each score >= thr
-//        appended to the query's candidate buffer. About rank / f appends
+//        appended to the query's candidate buffer (per lane half: one
+//        SADDR 8-byte store at the lane's cursor). About rank / f appends
 //        per query (~600 at the C4 shapes), against thousands for a running
-//        threshold that starts at -inf. Appends are staged per query in an LDS
-//        row and leave in 64-byte groups (one aligned write by the query's two
-//        lanes), not as scattered 8-byte stores. A buffer nearing its capacity
-//        is compacted by a radix select (threshold raised, never lowered).
+//        threshold that starts at -inf. A half nearing its capacity is
+//        compacted by the v2 radix compaction (threshold raised, never lowered).
 //        The filter of a set is a branch-free 16-bit pass mask (two VALU per
 //        score, scheduled into the next set's MFMA gaps) and a wave-uniform
 //        store loop that runs max-popcount times; the block barrier sits
@@ -43,7 +42,7 @@
 //        of the split buffers instead (< k entries: the query is flagged),
 //        and a rescue launch pair (mode 2) rebuilds the flagged queries from
 //        -inf while every other block exits at once.
-//    Each (split, query) writes its entry count to `meta`.
+//    Each (split, query, half) writes its entry count to `meta`.
 // 2. flatip_topk_v4_finish: one wave per query over the union of its split
 //    buffers: a radix select on the composite key (order-preserving score
 //    key << 32 | ~id, larger = better: score desc, id asc) down to <= 128
@@ -58,10 +57,8 @@ namespace topk {
 namespace v4 {
 
 constexpr int kWavesB = 8;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kCap = 1024;             // candidate entries per (split, query)
-constexpr int kGroup = 8;              // entries per staged flush: 64 bytes, one aligned half line
-constexpr int kStg = kGroup + 1;       // LDS slots per query row (72-byte stride: no bank conflicts)
+constexpr int kHalf = kCap / 2;        // per owning lane half
 constexpr int kMaxK = 128;
 constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
 constexpr int kMaxSplits = 8;
@@ -91,9 +88,7 @@ struct Cfg4 {
     static constexpr int TILE_BYTES = SLOTS * 16;
     static constexpr int RING = 3;
     static constexpr int HIST_BYTES = kWavesB * 1024;
-    // append staging: per (wave, query) one row of kStg Cand slots
-    static constexpr int STG_BYTES = kWavesB * kQS * 32 * kStg * 8;
-    static constexpr int LDS_BYTES = RING * TILE_BYTES + STG_BYTES + HIST_BYTES + 16;
+    static constexpr int LDS_BYTES = RING * TILE_BYTES + HIST_BYTES + 16;
     static_assert(PIECES * 64 == SLOTS, "whole DMA pieces");
     static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
@@ -213,42 +208,49 @@ __device__ __forceinline__ void radix_prefix(Each&& each, int k, int limit, uint
     }
 }
 
-// In-scan compaction of one query's buffer (n entries, k <= n), streamed from
-// memory so that the scan keeps its registers: keeps, in place and in order,
-// the entries in the radix bucket holding the k best (<= limit entries). thr =
-// the new filter threshold: the bucket's score floor (v >= thr), or, when the
-// bucket had to be resolved down into the ids (massive exact ties), strictly
-// above the k-th score — items arrive in increasing id order, so an equal
-// later score loses.
-__device__ __forceinline__ void compact_stream(Cand* __restrict__ buf, int& n, int k, int limit, uint32_t* hist,
-                                               float& thr) {
+// In-scan compaction of one query's buffer (halves of n0 / n1 entries, k <=
+// n0 + n1), streamed from memory so that the scan keeps its registers: each
+// half keeps, in place and in order, its entries in the radix bucket holding
+// the k best (<= limit entries in all). thr = the new filter threshold:
+// the bucket's score floor (v >= thr), or, when the bucket had to be resolved
+// down into the ids (massive exact ties), strictly above the k-th score — items
+// arrive in increasing id order, so an equal later score loses.
+__device__ __forceinline__ void compact_stream(Cand* __restrict__ buf, int& n0, int& n1, int k, int limit,
+                                               uint32_t* hist, float& thr) {
     const int lane = threadIdx.x & 63;
     __threadfence_block();
-    const int a0 = n;
+    const int a0 = n0, a1 = n1;
     auto each = [&](auto&& fn) {
         for (int i = lane; i < a0; i += 64) fn(ckey(buf[i]));
+        for (int i = lane; i < a1; i += 64) fn(ckey(buf[kHalf + i]));
     };
     uint64_t prefix = 0;
-    int shift = 64, kept = a0;
+    int shift = 64, kept = a0 + a1;
     radix_prefix(each, k, limit, hist, prefix, shift, kept);
     const uint64_t pmask = prefix_mask(shift);
-    int m = 0;
-    for (int i0 = 0; i0 < a0; i0 += 64) {
-        const int i = i0 + lane;
-        Cand c{-INFINITY, kEmptyId};
-        bool take = false;
-        if (i < a0) {
-            c = buf[i];
-            take = (ckey(c) & pmask) >= prefix;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Cand* p = buf + h * kHalf;
+        const int n = h ? a1 : a0;
+        int m = 0;
+        for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
+            Cand c{-INFINITY, kEmptyId};
+            bool take = false;
+            if (i < n) {
+                c = p[i];
+                take = (ckey(c) & pmask) >= prefix;
+            }
+            const uint64_t bm = __ballot(take);
+            const int pos = m + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                                    static_cast<uint32_t>(bm >> 32),
+                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bm), 0u)));
+            if (take) p[pos] = c;  // pos <= i: every lane read its entry before any lane writes
+            m += __popcll(bm);
         }
-        const uint64_t bm = __ballot(take);
-        const int pos = m + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-                                static_cast<uint32_t>(bm >> 32),
-                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bm), 0u)));
-        if (take) buf[pos] = c;  // pos <= i: every lane read its entry before any lane writes
-        m += __popcll(bm);
+        if (h) n1 = m;
+        else n0 = m;
     }
-    n = m;
     const float floor = v2::okey_inv(static_cast<uint32_t>(prefix >> 32));
     if (shift >= 32) thr = (static_cast<uint32_t>(prefix >> 32) <= 0x007FFFFFu) ? -FLT_MAX : floor;
     else thr = nextafterf(floor, INFINITY);
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     constexpr int QT = Geo<QS>::QT;
     __shared__ __attribute__((aligned(1024))) char lds[C::LDS_BYTES];
     char* const ring = lds;
-    uint32_t* const hist_all = reinterpret_cast<uint32_t*>(lds + C::RING * C::TILE_BYTES + C::STG_BYTES);
+    uint32_t* const hist_all = reinterpret_cast<uint32_t*>(lds + C::RING * C::TILE_BYTES);
     uint32_t* const flag = hist_all + kWavesB * 256;
 
     const T* __restrict__ Q = reinterpret_cast<const T*>(a.Q);
@@ -282,8 +284,6 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     const int64_t q_pad = static_cast<int64_t>(gridDim.x / splits) * QT;
     Cand* const cbase = a.cand + (static_cast<int64_t>(split) * q_pad + qw) * kCap;  // wave's 32·QS buffers
     uint32_t* const whist = hist_all + wave * 256;
-    // this wave's append staging rows: query j * 32 + col at stg_w + (j * 32 + col) * kStg
-    Cand* const stg_w = reinterpret_cast<Cand*>(lds + C::RING * C::TILE_BYTES) + wave * (kQS * 32 * kStg);
     const int nst = i_end > i_begin ? static_cast<int>((i_end - i_begin + C::NT - 1) / C::NT) : 0;
     // mode 0: per-split sample, per-split verification (rescan on failure);
     // mode 1 (joint): the sample pass covers the WHOLE corpus, so every split of
@@ -335,56 +335,31 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             asm volatile("" ::"v"(t.x), "v"(t.y), "v"(t.z), "v"(t.w));
         }
 
-    // ---- appends ----
-    // A query's entries go to its buffer (kCap entries per (split, query)) in
-    // groups of kGroup: each append is written to the query's LDS staging row
-    // (slot = count mod 8), and a completed group leaves as one 64-byte aligned
-    // write (two 32-byte stores, one per lane half). Scattered 8-byte stores
-    // into 1,024 buffers per block left as partial-line write-backs (round 4:
-    // 1.41 GB of scan writes per C4 call for 0.31 GB of appends).
-    // cnt[j]: the query's entry count (the same in both lane halves); entries
-    // [0, cnt & ~7) are in memory, [cnt & ~7, cnt) in the staging row.
+    // ---- append cursors: byte offset of the lane's next entry from the wave's base ----
     const uint32_t wb_lo = static_cast<uint32_t>(
         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase))));
     const uint32_t wb_hi = static_cast<uint32_t>(
         __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uint64_t>(cbase) >> 32)));
     const uint64_t wbase = (static_cast<uint64_t>(wb_hi) << 32) | wb_lo;
-    // wave-uniform global base: the group writes compile to SADDR global stores
+    // wave-uniform global base: the appends compile to SADDR global stores
+    // (a generic pointer would give flat stores, counted in lgkmcnt too)
     __attribute__((address_space(1))) char* const wbytes =
         reinterpret_cast<__attribute__((address_space(1))) char*>(wbase);
-    uint32_t goff[QS], cnt[QS];
+    uint32_t woff0[QS], woff[QS];
     float thr[QS];
 #pragma unroll
     for (int j = 0; j < QS; ++j) {
-        goff[j] = static_cast<uint32_t>((j * 32 + col) * kCap * sizeof(Cand)) + 32u * half;  // this half's 32 bytes
-        cnt[j] = 0u;
+        woff0[j] = static_cast<uint32_t>(((j * 32 + col) * kCap + half * kHalf) * sizeof(Cand));
+        woff[j] = woff0[j];
         thr[j] = qok[j] ? -FLT_MAX : INFINITY;
     }
     if (mode == 2) {  // rescue: the flagged queries from -inf (a running threshold), the rest skip
 #pragma unroll
         for (int j = 0; j < QS; ++j) thr[j] = (qok[j] && fail[qw + j * 32 + col] != 0) ? -FLT_MAX : INFINITY;
     }
-    constexpr int kHead = C::NSUB * 32;  // appends per query between two compaction checks, at most
-    constexpr int kLimit = kCap - kHead;  // a compaction keeps at most this many entries
-    // group g of query set j (this lane's half of it): staging row -> memory
-    auto flush_group = [&](int j, uint32_t g) {
-        const Cand* r = stg_w + (j * 32 + col) * kStg + 4 * half;
-        const uint2 e0 = *reinterpret_cast<const uint2*>(r), e1 = *reinterpret_cast<const uint2*>(r + 1);
-        const uint2 e2 = *reinterpret_cast<const uint2*>(r + 2), e3 = *reinterpret_cast<const uint2*>(r + 3);
-        auto* gp = reinterpret_cast<__attribute__((address_space(1))) u32x4*>(wbytes + goff[j] + g * (kGroup * 8u));
-        gp[0] = u32x4{e0.x, e0.y, e1.x, e1.y};
-        gp[1] = u32x4{e2.x, e2.y, e3.x, e3.y};
-    };
-    // memory -> staging row (after a compaction left a partial last group)
-    auto load_group = [&](int j, uint32_t g) {
-        Cand* r = stg_w + (j * 32 + col) * kStg + 4 * half;
-        const auto* gp = reinterpret_cast<const __attribute__((address_space(1))) u32x4*>(wbytes + goff[j] + g * (kGroup * 8u));
-        const u32x4 a0 = gp[0], a1 = gp[1];
-        *reinterpret_cast<uint2*>(r) = make_uint2(a0.x, a0.y);
-        *reinterpret_cast<uint2*>(r + 1) = make_uint2(a0.z, a0.w);
-        *reinterpret_cast<uint2*>(r + 2) = make_uint2(a1.x, a1.y);
-        *reinterpret_cast<uint2*>(r + 3) = make_uint2(a1.z, a1.w);
-    };
+    constexpr int kHead = C::NSUB * 16;  // appends per half between two compaction checks, at most
+    constexpr uint32_t kLimBytes = static_cast<uint32_t>((kHalf - kHead) * sizeof(Cand));
+    constexpr int kLimit = kHalf - kHead;  // a compaction keeps at most this many entries (in all)
 
     // ---- DMA plan (as v3): this wave's pieces w, w+8, ... of a stage ----
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -476,13 +451,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     };
     auto store_loop = [&](int j, uint32_t pm, const f32x16& acc, int64_t sub0) {
         const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
-        Cand* const row = stg_w + (j * 32 + col) * kStg;
-        uint32_t c = cnt[j];
+        uint32_t wo = woff[j];
         while (__ballot(pm != 0u)) {
-            const bool take = pm != 0u;
-            float s = 0.0f;
-            uint32_t id = 0u;
-            if (take) {
+            issued += 1;  // exactly one store instruction (dwordx2) for the wave
+            if (pm) {
                 // the lowest passing row as an isolated bit, tested against
                 // constant masks; the score is picked by explicit v_cndmask
                 // instructions (written as selects on acc[], the compiler folds
@@ -499,26 +471,15 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
                 for (int i = 0; i < 4; ++i) v4[i] = lane_sel(m1, v8[2 * i], v8[2 * i + 1]);
 #pragma unroll
                 for (int i = 0; i < 2; ++i) v2[i] = lane_sel(m2, v4[2 * i], v4[2 * i + 1]);
-                s = lane_sel(m3, v2[0], v2[1]);
-                id = sub_lane + (b0 ? 1u : 0u) + (b1 ? 2u : 0u) + (b2 ? 8u : 0u) + (b3 ? 16u : 0u);
+                const float s = lane_sel(m3, v2[0], v2[1]);
+                const uint32_t id = sub_lane + (b0 ? 1u : 0u) + (b1 ? 2u : 0u) + (b2 ? 8u : 0u) + (b3 ? 16u : 0u);
+                // a compiler-visible SADDR store (hipcc counts it and pads its hazards)
+                *reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(wbytes + wo) =
+                    (static_cast<uint64_t>(id) << 32) | __float_as_uint(s);
+                wo += 8;
             }
-            // the query's two lanes append in half order: half 1 after half 0
-            const uint64_t bm = __ballot(take);
-            const uint32_t pt = static_cast<uint32_t>(bm >> (lane ^ 32)) & 1u;  // the partner lane appends
-            const uint32_t pos = c + (half ? pt : 0u);
-            const uint32_t nc = c + (take ? 1u : 0u) + pt;
-            const bool spill = (pos ^ c) >= kGroup;  // this entry opens the next group
-            if (take && !spill) row[pos & (kGroup - 1)] = Cand{s, id};
-            const bool full = (nc ^ c) >= kGroup;  // group c / 8 is complete
-            if (__ballot(full)) {
-                wave_lds_sync();  // the partner's slot writes are visible
-                if (full) flush_group(j, c / kGroup);
-                issued += 2;  // two store instructions for the wave
-            }
-            if (take && spill) row[0] = Cand{s, id};
-            c = nc;
         }
-        cnt[j] = c;
+        woff[j] = wo;
     };
     // rows of a sub-tile with `left` (< 32) valid rows, as this lane's pass-mask bits
     auto tail_bits = [&](int left) -> uint32_t {
@@ -536,31 +497,21 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     auto maybe_compact = [&]() {
 #pragma unroll
         for (int j = 0; j < QS; ++j) {
-            const uint64_t m = __ballot(cnt[j] > static_cast<uint32_t>(kLimit));
+            const uint64_t m = __ballot(woff[j] - woff0[j] > kLimBytes);
             uint32_t need = static_cast<uint32_t>(m) | static_cast<uint32_t>(m >> 32);
             if (!need) continue;
             while (need) {
-                const int q = __builtin_ctz(need);
+                const int c = __builtin_ctz(need);
                 need &= need - 1;
-                const uint32_t n0 = __shfl(cnt[j], q, 64);
-                if (n0 % kGroup) {  // the staged partial group goes to memory first
-                    wave_lds_sync();
-                    if (col == q) flush_group(j, n0 / kGroup);
-                }
-                int n = static_cast<int>(n0);
+                const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
+                int n0 = __shfl(cnt, c, 64), n1 = __shfl(cnt, c + 32, 64);
                 float nt;
-                compact_stream(cbase + static_cast<int64_t>(j * 32 + q) * kCap, n, k, kLimit, whist, nt);
-                const uint32_t n1 = static_cast<uint32_t>(n);
-                if (n1 % kGroup) {  // its new partial group back to the staging row
-                    if (col == q) load_group(j, n1 / kGroup);
-                    wave_lds_sync();
-                }
-                if (col == q) {
-                    cnt[j] = n1;
+                compact_stream(cbase + static_cast<int64_t>(j * 32 + c) * kCap, n0, n1, k, kLimit, whist, nt);
+                if (col == c) {
+                    woff[j] = woff0[j] + static_cast<uint32_t>((half ? n1 : n0) * sizeof(Cand));
                     thr[j] = fmaxf(thr[j], nt);
                 }
             }
-            __threadfence_block();
 #pragma unroll
             for (int i = 0; i < C::RING - 1; ++i) mk[i] = issued;  // drained
         }
@@ -800,11 +751,13 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         bool any = false;
 #pragma unroll
         for (int j = 0; j < QS; ++j) {
-            const bool fail = qok[j] && static_cast<int>(cnt[j]) < k;
+            const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
+            const int tot = cnt + __shfl_xor(cnt, 32, 64);
+            const bool fail = qok[j] && tot < k;
             any |= fail;
             if (fail) {
                 thr[j] = -FLT_MAX;  // start over for this query: empty buffer, v2 selection
-                cnt[j] = 0u;
+                woff[j] = woff0[j];
             } else {
                 thr[j] = INFINITY;  // done: no appends in the rescan
             }
@@ -814,12 +767,11 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         if (*flag) main_pass();  // block-uniform
     }
 
-    // ---- the staged partial groups, and the entry counts for the finish pass ----
-    wave_lds_sync();
+    // ---- entry counts for the finish pass ----
 #pragma unroll
     for (int j = 0; j < QS; ++j) {
-        if (cnt[j] % kGroup) flush_group(j, cnt[j] / kGroup);
-        if (half == 0) meta[(static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col] = static_cast<int>(cnt[j]);
+        const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
+        meta[((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * 2 + half] = cnt;
     }
 #ifdef RT_TOPK_PROBE_TIMING
     {  // [total, DMA wait, barrier, main sub-tiles, sample pass, compaction checks]
@@ -875,10 +827,10 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
     if (mode == 2 && fail[q] == 0) return;
     uint32_t* hist = hist_all[w];
     Cand* keep = keep_all[w];
-    const int nseg = splits;
-    // segment (split s) = lane s: entry count and inclusive prefix
+    const int nseg = 2 * splits;
+    // segment (split s, half h) = lane 2s+h: entry count and exclusive prefix
     int cnt = 0;
-    if (lane < nseg) cnt = meta[static_cast<int64_t>(lane) * q_pad + q];
+    if (lane < nseg) cnt = meta[((static_cast<int64_t>(lane >> 1) * q_pad) + q) * 2 + (lane & 1)];
     int pre = cnt;  // inclusive prefix over lanes
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -895,7 +847,7 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
         if (short_) return;
     }
     auto seg_ptr = [&](int sg) {
-        return cand + (static_cast<int64_t>(sg) * q_pad + q) * kCap;
+        return cand + ((static_cast<int64_t>(sg >> 1) * q_pad) + q) * kCap + (sg & 1) * kHalf;
     };
     // visit every entry: fn(entry); segments in order, lanes strided
     auto each = [&](auto&& fn) {
@@ -915,13 +867,13 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
         // the bits all keys share (scores above one threshold agree in sign,
         // exponent and the top mantissa bits), so its first pass already
         // splits them, and no pass re-reads memory.
-        int bnd[kMaxSplits];  // inclusive segment ends (wave-uniform)
+        int bnd[2 * kMaxSplits];  // inclusive segment ends (wave-uniform)
 #pragma unroll
-        for (int t = 0; t < kMaxSplits; ++t) bnd[t] = __builtin_amdgcn_readlane(pre, t);
+        for (int t = 0; t < 2 * kMaxSplits; ++t) bnd[t] = __builtin_amdgcn_readlane(pre, t);
         uint64_t key[kFinishRegs];
         uint64_t mx = 0ull, mn = ~0ull;
         // all loads issued before any is used; the segment of slot f found by
-        // a search over NS - 1 boundaries (NS = 2: the 2-split C4 plans)
+        // a search over NS - 1 boundaries (NS = 4: the 2-split C4 plans)
         auto load_all = [&](auto ns_tag) {
             constexpr int NS = decltype(ns_tag)::value;
 #pragma unroll
@@ -937,8 +889,8 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
                 }
             }
         };
-        if (nseg <= 2) load_all(std::integral_constant<int, 2>{});
-        else load_all(std::integral_constant<int, kMaxSplits>{});
+        if (nseg <= 4) load_all(std::integral_constant<int, 4>{});
+        else load_all(std::integral_constant<int, 2 * kMaxSplits>{});
 #pragma unroll
         for (int e = 0; e < kFinishRegs; ++e) {
             if (e * 64 + lane < total) {

@@ -11,10 +11,11 @@
   reduction runs over D, so the merged result is identical to one GPU holding
   the whole corpus.
 * Table-sharded row gather (config C5): the owner of row ``id`` is the rank
-  whose contiguous range holds it; the batch ids are all-gathered, every rank
-  gathers the whole batch against its own window (zero rows elsewhere) and one
-  byte-wise MAX all-reduce leaves every owner's rows everywhere (copies only,
-  no host synchronisation, graph-capturable).
+  whose row window holds it; the batch ids and the windows are all-gathered
+  together, each owner packs its positions' rows into a fixed-size segment and
+  one all-gather of the segments leaves every row everywhere (a skewed batch
+  that overflows a segment, and hipGraph capture, take the sync-free byte-wise
+  MAX all-reduce instead).
 * Data-parallel in-batch step of config C5 (:func:`sharded_inbatch_step`):
   each rank scores its own users against the whole gathered batch of items;
   the table is frozen as in the reference (no item-gradient exchange), or, for
@@ -157,42 +158,121 @@ def _batch_counts(ids: torch.Tensor, counts: Optional[Sequence[int]], uniform: b
     return [int(c) for c in sizes.tolist()]
 
 
-def _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform):
+def segment_capacity(positions: int, world: int) -> int:
+    """Rows per owner segment of the owner-segment exchange: the mean share
+    P/N plus 8 standard deviations of a uniform batch's per-owner count
+    (Binomial(P, 1/N)), rounded up to 64 and capped at P (then no batch can
+    overflow). At C5 (P = 65,536, N = 8): 8,896 rows = 1.09 P/N."""
+    if world <= 1 or positions <= 0:
+        return max(positions, 0)
+    mean = positions / world
+    sd = (positions * (1.0 / world) * (1.0 - 1.0 / world)) ** 0.5
+    cap = int(-(-(mean + 8.0 * sd) // 64) * 64)
+    return min(cap, positions)
+
+
+def _capturing(t: torch.Tensor) -> bool:
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
+
+
+class _Owners:
+    """Ownership of the global batch positions, computed identically on every
+    rank from the all-gathered ids and row windows (device tensors, no host
+    read): ``inwin`` [P, N] position p lies in rank r's window; ``valid`` [P];
+    ``own`` [P] (0 where invalid); ``slot`` [P] = rank of p among its owner's
+    positions (batch order); ``counts`` [N]."""
+
+    def __init__(self, all_ids: torch.Tensor, windows: torch.Tensor):
+        beg, end = windows[:, 0], windows[:, 1]
+        ids = all_ids.unsqueeze(1)
+        self.inwin = (ids >= beg.unsqueeze(0)) & (ids < end.unsqueeze(0))
+        self.valid = self.inwin.any(dim=1)
+        self.own = self.inwin.to(torch.int8).argmax(dim=1)
+        cs = self.inwin.to(torch.int32).cumsum(0)
+        self.counts = cs[-1] if cs.shape[0] else torch.zeros(windows.shape[0], dtype=torch.int32,
+                                                            device=all_ids.device)
+        self.slot = cs.gather(1, self.own.unsqueeze(1)).squeeze(1).to(torch.int64) - 1
+
+
+def _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform, exchange="auto"):
     """Shared body of :func:`sharded_gather_rows`: (rows of the global batch,
-    global ids, this rank's count of positions it owns (int64 [1], device, NOT
-    reduced over ranks), number of valid positions)."""
+    global ids, number of positions owned by some rank (int64 [1], device,
+    global), number of valid positions, exchange record (dict))."""
     gather_fn = gather
-    oob = None
     if gather_fn is None:
-        oob = torch.zeros(1, dtype=torch.int32, device=ids.device)
-        gather_fn = lambda t, i, b: kernels.gather_rows(t, i, row_begin=b, oob=oob)  # noqa: E731
+        gather_fn = lambda t, i, b: kernels.gather_rows(t, i, row_begin=b)  # noqa: E731
     world, rank = _world(group)
     ids = ids.to(torch.int64)
     counts = _batch_counts(ids, counts, uniform, group, world, rank)
     width = max(counts) if counts is not None else ids.numel()
-    if world > 1:
-        padded = ids
-        if ids.numel() != width:
-            padded = torch.full((width,), -1, dtype=torch.int64, device=ids.device)
-            padded[: ids.numel()] = ids
-        all_ids = torch.empty((world * width,), dtype=torch.int64, device=ids.device)
-        dist.all_gather_into_tensor(all_ids, padded.contiguous(), group=group)
-    else:
-        all_ids = ids
-    rows = gather_fn(table_shard, all_ids, row_begin)
     n_valid = sum(counts) if counts is not None else world * width
-    if oob is not None:
-        owned = all_ids.numel() - oob.to(torch.int64)
-    else:
+    dev = ids.device
+    rec = {"mode": "local", "bytes_per_rank": 0}
+    if world == 1:
+        all_ids = ids
+        rows = gather_fn(table_shard, all_ids, row_begin)
         loc = all_ids - int(row_begin)
         owned = ((loc >= 0) & (loc < table_shard.shape[0])).sum().reshape(1)
-    if world > 1:
-        rows = _exchange_rows(rows, group)
+        return rows, all_ids, owned, n_valid, rec
+    # ids (padded to the batch width with -1) and the rank's row window in ONE all-gather
+    send = torch.full((width + 2,), -1, dtype=torch.int64, device=dev)
+    send[: ids.numel()] = ids
+    send[width] = int(row_begin)
+    send[width + 1] = int(row_begin) + int(table_shard.shape[0])
+    recv = torch.empty((world * (width + 2),), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(recv, send, group=group)
+    recv = recv.view(world, width + 2)
+    all_ids = recv[:, :width].reshape(-1)
+    own = _Owners(all_ids, recv[:, width:])
+    owned = own.valid.sum().reshape(1).to(torch.int64)
+    P, D = all_ids.numel(), table_shard.shape[1]
+    esz = table_shard.element_size()
+    ids_bytes = (world - 1) * (width + 2) * 8
+    if exchange == "auto":
+        exchange = "max" if _capturing(ids) else "segments"
+    rows = None
+    if exchange == "segments":
+        cap = segment_capacity(P, world)
+        ovf = (own.counts > cap).any().reshape(1)
+        flag = None
+        if cap < P:  # an overflow is possible: fetch the flag early (the collectives below run meanwhile)
+            flag = torch.empty(1, dtype=torch.bool, pin_memory=dev.type == "cuda")
+            flag.copy_(ovf, non_blocking=True)
+            ev = torch.cuda.Event() if dev.type == "cuda" else None
+            if ev is not None:
+                ev.record()
+        # this rank's owned positions, in batch order, packed into its segment
+        mine = own.valid & (own.own == rank) & (own.slot < cap)
+        seg_ids = torch.full((cap + 1,), -1, dtype=torch.int64, device=dev)
+        seg_ids.scatter_(0, torch.where(mine, own.slot, cap), all_ids)
+        seg_rows = gather_fn(table_shard, seg_ids[:cap], row_begin).contiguous()
+        all_seg = torch.empty((world * cap, D), dtype=seg_rows.dtype, device=dev)
+        dist.all_gather_into_tensor(all_seg, seg_rows, group=group)
+        src = torch.where(own.valid & (own.slot < cap), own.own.to(torch.int64) * cap + own.slot,
+                          torch.full_like(own.slot, -1))
+        rows = gather_fn(all_seg, src, 0)
+        if flag is not None:
+            if dev.type == "cuda":
+                ev.synchronize()
+            if bool(flag[0]):  # skewed batch: some owner holds more than cap positions
+                rows = None
+                exchange = "max"
+            else:
+                rec = {"mode": "owner segments", "segment_rows": cap,
+                       "bytes_per_rank": ids_bytes + (world - 1) * cap * D * esz}
+        else:
+            rec = {"mode": "owner segments", "segment_rows": cap,
+                   "bytes_per_rank": ids_bytes + (world - 1) * cap * D * esz}
+    if rows is None:
+        # sync-free fallback: every rank gathers the global batch against its
+        # own window (zero rows elsewhere), one byte-wise MAX all-reduce
+        rows = _exchange_rows(gather_fn(table_shard, all_ids, row_begin), group)
+        rec = {"mode": "byte-MAX all-reduce", "bytes_per_rank": ids_bytes + 2 * (world - 1) * P * D * esz // world}
     if counts is not None and any(c != width for c in counts):  # drop the padding (host-known positions)
-        keep = torch.cat([torch.arange(r * width, r * width + c, device=ids.device) for r, c in enumerate(counts)])
+        keep = torch.cat([torch.arange(r * width, r * width + c, device=dev) for r, c in enumerate(counts)])
         rows = rows.index_select(0, keep)
         all_ids = all_ids.index_select(0, keep)
-    return rows, all_ids, owned, n_valid
+    return rows, all_ids, owned, n_valid, rec
 
 
 def _status_update(status: Optional[torch.Tensor], check: bool, n_valid: int, owned_total: torch.Tensor):
@@ -206,40 +286,54 @@ def _status_update(status: Optional[torch.Tensor], check: bool, n_valid: int, ow
         raise IndexError("batch id outside every rank's table window")
 
 
+LAST_EXCHANGE: dict = {}  # the record of the latest row exchange (mode, segment rows, bytes per rank)
+
+
 def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Tensor, group=None,
                         gather: Optional[Callable] = None, counts: Optional[Sequence[int]] = None,
                         status: Optional[torch.Tensor] = None, check: bool = False,
-                        return_ids: bool = False, uniform: bool = False):
+                        return_ids: bool = False, uniform: bool = False, exchange: str = "auto"):
     """C5 row fetch from a row-sharded table: returns the rows of the GLOBAL
     batch (all ranks' ``ids`` concatenated in rank order) on every rank.
 
-    One all-gather of the batch ids (each rank's ids padded to the batch width
-    with -1); every rank gathers the WHOLE global batch against its own row
-    window (``rt_gather_rows`` with ``row_begin``: ids outside the window, and
-    the -1 padding, give zero rows and are counted as out-of-window); one
-    all-reduce of the rows' bytes (:func:`_exchange_rows`) leaves every
-    position holding its owner's row. Rows are copied, never summed, so the
-    result is bit-identical to a single-table gather.
+    One all-gather carries the batch ids (each rank's padded to the batch width
+    with -1) together with every rank's row window, so every rank knows which
+    rank owns each position (identically, on the device). Then, ``exchange``:
+
+    * ``"segments"`` (the default outside hipGraph capture): each owner packs
+      its positions' rows, in batch order, into a fixed segment of
+      :func:`segment_capacity` rows (≈ 1.09·P/N at C5) and ONE all-gather of
+      the segments delivers them; every rank places them by (owner, slot). Per
+      rank that moves (N-1)·cap·D·esz bytes, against 2(N-1)/N·P·D·esz for the
+      all-reduce below (about 0.55× at N = 8). The only host read is the
+      overflow flag (some owner holds more positions than a segment), fetched
+      while the all-gather runs; an overflowing (skewed) batch re-runs the
+      exchange as ``"max"``.
+    * ``"max"`` (the default while capturing; sync-free): every rank gathers the
+      WHOLE global batch against its own row window (zero rows outside it) and
+      one all-reduce of the rows' bytes (:func:`_exchange_rows`) leaves every
+      position holding its owner's row.
+
+    Rows are copied, never summed, so the result is bit-identical to a
+    single-table gather. The exchange's mode and bytes per rank are kept in
+    ``LAST_EXCHANGE``.
 
     Batch sizes: ``counts`` (host data, one entry per rank) when the caller
     knows them; ``uniform=True`` when every rank holds the same number of ids
-    (the C5 step) — then no device→host read happens anywhere and the call can
-    be captured in a hipGraph; otherwise the sizes are all-gathered first (one
-    tiny collective and a host read), so ragged batches always work.
+    (the C5 step); otherwise the sizes are all-gathered first (one tiny
+    collective and a host read), so ragged batches always work.
 
-    Id-range check: the positions owned by some rank are counted on the device
-    and summed over ranks by one 8-byte all-reduce that EVERY rank runs
-    (whatever ``status``/``check`` it passes, so mismatched arguments cannot
-    deadlock). ``status`` (int64 [2], device, optional) accumulates
-    (positions, owned positions); they differ iff some id lies outside every
-    window. ``check=True`` reads them and raises IndexError (one sync).
-    ``gather(table, ids, row_begin)`` returns [len(ids), dim] with zero rows
-    outside the window, as ``rt_gather_rows`` does (the default).
+    Id-range check: every rank counts the positions owned by some rank from the
+    gathered windows (no extra collective). ``status`` (int64 [2], device,
+    optional) accumulates (positions, owned positions); they differ iff some id
+    lies outside every window. ``check=True`` reads them and raises IndexError
+    (one sync). ``gather(table, ids, row_begin)`` returns [len(ids), dim] with
+    zero rows outside the window, as ``rt_gather_rows`` does (the default).
     ``return_ids``: also return the global ids (-1 padding removed)."""
-    world, _ = _world(group)
-    rows, all_ids, owned, n_valid = _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform)
-    if world > 1:
-        dist.all_reduce(owned, op=dist.ReduceOp.SUM, group=group)
+    rows, all_ids, owned, n_valid, rec = _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform,
+                                                        exchange)
+    LAST_EXCHANGE.clear()
+    LAST_EXCHANGE.update(rec)
     _status_update(status, check, n_valid, owned)
     return (rows, all_ids) if return_ids else rows
 
@@ -247,7 +341,8 @@ def sharded_gather_rows(table_shard: torch.Tensor, row_begin: int, ids: torch.Te
 def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_ids: torch.Tensor,
                              grad_rows: torch.Tensor, group=None,
                              scatter_add: Optional[Callable] = None,
-                             status: Optional[torch.Tensor] = None, check: bool = False) -> torch.Tensor:
+                             status: Optional[torch.Tensor] = None, check: bool = False,
+                             exchange: str = "auto") -> torch.Tensor:
     """Backward of :func:`sharded_gather_rows` for a TRAINABLE row-sharded table
     (the nn.Embedding path a2 under C5 sharding, SURVEY §8(e) "next"): every rank
     holds its own contribution to d loss / d rows for the whole global batch
@@ -255,49 +350,73 @@ def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_id
     of each row adds the sum over ranks into its shard's gradient
     (``grad_shard`` [rows, D], shard rows start at global ``row_begin``).
 
-    Sync-free: one all-reduce (sum, fp32) of the row gradients, then every rank
-    scatter-adds the rows of its own window (``rt_scatter_add_rows_f32`` skips
-    ids outside [0, rows); repeated ids accumulate). The all-reduce moves
-    2(N-1)/N · B_total·D·4 bytes per rank; an owner reduce-scatter moves half
-    that but needs the per-owner counts on the host (a sync) or fixed padded
-    owner segments of B_total rows each (N/2 times MORE bytes), so the
-    all-reduce is the sync-free optimum here.
+    One all-gather of the row windows (16 bytes per rank) tells every rank the
+    owner of each position. ``exchange``:
 
-    Id-range check without an extra collective: this rank's count of ids inside
-    its window rides in one extra row of the same all-reduce (exact in fp32 for
-    B_total < 2^24), so the sum is the number of positions owned by some rank.
-    ``status`` (int64 [2]) accumulates (positions, owned positions); ``check``
-    raises IndexError when they differ (one sync)."""
+    * ``"segments"`` (default outside capture): each rank lays its row
+      gradients out as N owner segments of :func:`segment_capacity` rows (batch
+      order within an owner) and ONE reduce-scatter leaves each owner the sum
+      over ranks of its own segment, which it scatter-adds into its shard:
+      (N-1)·cap·D·4 bytes per rank, about half of the all-reduce below. The
+      overflow flag (a skewed batch) is read on the host; an overflow re-runs
+      as ``"allreduce"``.
+    * ``"allreduce"`` (sync-free): one all-reduce (sum, fp32) of the whole
+      [B_total, D] gradient, then every rank scatter-adds the rows of its own
+      window (``rt_scatter_add_rows_f32`` skips ids outside [0, rows)).
+
+    Repeated ids accumulate. ``status`` (int64 [2]) accumulates (positions,
+    owned positions); ``check`` raises IndexError when they differ (one sync)."""
     scatter_add = scatter_add or (lambda t, ids, g: kernels.scatter_add_rows(t, ids, g))
-    world, _ = _world(group)
+    world, rank = _world(group)
     gids = global_ids.to(torch.int64)
     loc = gids - int(row_begin)
     n_pos = gids.numel()
-    track = status is not None or check
-    if track and n_pos >= (1 << 24):
-        raise ValueError("status/check count positions in fp32: B_total must be < 2^24")
     d = grad_rows.shape[-1]
-    if world > 1 or track:
-        g = torch.zeros((n_pos + 1, d), dtype=torch.float32, device=grad_rows.device)
-        g[:n_pos] = grad_rows.reshape(n_pos, d)
-        g[n_pos, 0] = ((loc >= 0) & (loc < grad_shard.shape[0])).sum().to(torch.float32)
-        if world > 1:
-            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
-        owned = g[n_pos, 0].round().to(torch.int64)
-        g = g[:n_pos]
-    else:
-        g = grad_rows
-        owned = None
+    g = grad_rows.reshape(n_pos, d)
+    dev = g.device
+    track = status is not None or check
+    if world == 1:
+        if track:
+            owned = ((loc >= 0) & (loc < grad_shard.shape[0])).sum().reshape(1)
+            _status_update(status, check, n_pos, owned)
+        return scatter_add(grad_shard, loc, g)
+    win = torch.tensor([int(row_begin), int(row_begin) + int(grad_shard.shape[0])], dtype=torch.int64, device=dev)
+    wins = torch.empty((world * 2,), dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(wins, win, group=group)
+    own = _Owners(gids, wins.view(world, 2))
     if track:
-        _status_update(status, check, n_pos, owned)
-    return scatter_add(grad_shard, loc, g)
+        _status_update(status, check, n_pos, own.valid.sum().reshape(1))
+    if exchange == "auto":
+        exchange = "allreduce" if _capturing(g) else "segments"
+    if exchange == "segments":
+        cap = segment_capacity(n_pos, world)
+        if cap >= n_pos or not bool((own.counts > cap).any()):
+            dst = torch.where(own.valid & (own.slot < cap), own.own.to(torch.int64) * cap + own.slot,
+                              torch.full_like(own.slot, world * cap))
+            send = torch.zeros((world * cap + 1, d), dtype=torch.float32, device=dev)
+            send.index_put_((dst,), g.float(), accumulate=False)  # invalid positions -> the dummy last row
+            mine_seg = torch.empty((cap, d), dtype=torch.float32, device=dev)
+            dist.reduce_scatter_tensor(mine_seg, send[: world * cap].contiguous(), group=group)
+            # this owner's segment ids (batch order), local to the shard; padding -> -1 (skipped)
+            mine = own.valid & (own.own == rank) & (own.slot < cap)
+            seg_loc = torch.full((cap + 1,), -1, dtype=torch.int64, device=dev)
+            seg_loc.scatter_(0, torch.where(mine, own.slot, cap), loc)
+            LAST_EXCHANGE.clear()
+            LAST_EXCHANGE.update({"mode": "owner reduce-scatter", "segment_rows": cap,
+                                  "bytes_per_rank": 16 * (world - 1) + (world - 1) * cap * d * 4})
+            return scatter_add(grad_shard, seg_loc[:cap], mine_seg)
+    ga = g.float().contiguous().clone()
+    dist.all_reduce(ga, op=dist.ReduceOp.SUM, group=group)
+    LAST_EXCHANGE.clear()
+    LAST_EXCHANGE.update({"mode": "all-reduce", "bytes_per_rank": 16 * (world - 1) + 2 * (world - 1) * n_pos * d * 4 // world})
+    return scatter_add(grad_shard, loc, ga)
 
 
 def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: torch.Tensor,
                          item_ids: torch.Tensor, temperature: float, group=None,
                          gather: Optional[Callable] = None, loss_fn: Optional[Callable] = None,
                          grad_shard: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None,
-                         scatter_add: Optional[Callable] = None):
+                         scatter_add: Optional[Callable] = None, exchange: str = "auto"):
     """Config C5 data-parallel in-batch step (SURVEY §8(e) training): the item
     table is row-sharded, every rank holds ``user_emb`` [b, D] for its own b
     users and ``item_ids`` [b] of their positives (b equal on every rank). The
@@ -305,32 +424,37 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     :func:`sharded_gather_rows` (``uniform``: equal batches); each rank scores
     its users against ALL gathered items (label of local user i = global item
     rank·b + i) with ``rt_inbatch_loss_fwd_bwd``; the loss is averaged over
-    ranks by one 16-byte all-reduce that also carries the owned-position
-    count of the id-range check (``status``), so the step runs exactly three
-    collectives: ids all-gather, row MAX all-reduce, (loss, owned) all-reduce.
+    ranks by one 8-byte all-reduce. The step runs three collectives: the
+    ids + windows all-gather, the segment all-gather (``exchange``, see
+    :func:`sharded_gather_rows`), the loss all-reduce.
 
     The item table is a frozen feature table in the reference
     (src/training/datasets/movielens.py:61-63,116), so by default the item-row
     gradients are NOT exchanged: the third result is this rank's own
     contribution [B_total, D]. With ``grad_shard`` (a trainable table) they are
     summed and added into the owners' shards (:func:`sharded_scatter_add_rows`).
-    No host synchronisation at any world size, N = 1 included (the same code
-    runs; its collectives are skipped), so the whole step can be captured in a
-    hipGraph. Returns (global mean loss [1], d loss/d user_emb, d loss/d rows
-    (this rank's part))."""
+    At N = 1 the same code runs with its collectives skipped. The segment
+    exchange reads one overflow flag on the host; under hipGraph capture (or
+    ``exchange="max"``) the step is sync-free. Returns (global mean loss [1],
+    d loss/d user_emb, d loss/d rows (this rank's part))."""
     world, rank = _world(group)
     b = user_emb.shape[0]
-    rows, gids, owned, n_valid = _gather_global(table_shard, row_begin, item_ids, group, gather, None, True)
+    rows, gids, owned, n_valid, rec = _gather_global(table_shard, row_begin, item_ids, group, gather, None, True,
+                                                     exchange)
+    LAST_EXCHANGE.clear()
+    LAST_EXCHANGE.update(rec)
     loss_fn = loss_fn or (lambda u, p, off: kernels.inbatch_loss(u, p, temperature, label_offset=off))
     loss, du, dp = loss_fn(user_emb, rows, rank * b)
-    red = torch.cat([loss[0:1].to(torch.float64), owned.to(torch.float64).reshape(1).to(loss.device)])
+    lv = loss[0:1]
     if world > 1:
-        dist.all_reduce(red, op=dist.ReduceOp.SUM, group=group)
-    lv = red[0:1].to(loss.dtype)  # the loss kernel's dtype (the reduction ran in fp64)
+        lv = lv.to(torch.float64, copy=True)
+        dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
+        lv = lv.to(loss.dtype)  # the loss kernel's dtype (the reduction ran in fp64)
     if status is not None:
-        _status_update(status, False, n_valid, red[1].round().to(torch.int64))
+        _status_update(status, False, n_valid, owned)
     if grad_shard is not None:
-        sharded_scatter_add_rows(grad_shard, row_begin, gids, dp.float() / world, group, scatter_add)
+        sharded_scatter_add_rows(grad_shard, row_begin, gids, dp.float() / world, group, scatter_add,
+                                 exchange=("allreduce" if exchange == "max" else exchange))
     # each rank's loss is a mean over its own b users; the global mean averages them
     return lv / world, du / world, dp / world
 

@@ -19,9 +19,9 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import flat_ip as orc
-from rtrec_amd.dist.sharded import (allreduce_mean_, owner_of, shard_range, sharded_gather_rows, sharded_inbatch_step,
-                                    sharded_scatter_add_rows,
-                               sharded_topk, sharded_topk_owner)
+from rtrec_amd.dist import sharded as sharded_mod
+from rtrec_amd.dist.sharded import (allreduce_mean_, owner_of, segment_capacity, shard_range, sharded_gather_rows,
+                                    sharded_inbatch_step, sharded_scatter_add_rows, sharded_topk, sharded_topk_owner)
 
 
 def _free_port():
@@ -150,6 +150,16 @@ def _gather_worker(rank, world, n, d, seed, counts, skew):
     ref = table[np.concatenate(all_ids)]
     np.testing.assert_array_equal(rows.numpy(), ref)
     assert status[0] == status[1] == sum(counts)  # every id owned by exactly one rank
+    # owner segments unless a skewed batch overflowed one (then the byte-MAX exchange)
+    P = world * max(counts)
+    cap = segment_capacity(P, world)
+    overflow = skew and cap < P and max(counts) > 0 and sum(counts) > cap
+    want = "byte-MAX all-reduce" if overflow else "owner segments"
+    assert sharded_mod.LAST_EXCHANGE["mode"] == want, (sharded_mod.LAST_EXCHANGE, cap, P)
+    for mode in ("max", "segments"):  # both exchanges, forced, give the same rows
+        r = sharded_gather_rows(shard, b, torch.from_numpy(all_ids[rank]), gather=window_gather,
+                                counts=counts if len(set(counts)) > 1 else None, exchange=mode)
+        np.testing.assert_array_equal(r.numpy(), ref)
     # bit-exact through the byte-wise exchange: -0.0 and NaN payloads survive
     special = table.copy()
     special[::7, 0] = -0.0
@@ -191,18 +201,22 @@ def _gather_worker(rank, world, n, d, seed, counts, skew):
 
 
 @pytest.mark.parametrize("world,counts,skew", [(2, [13, 29], False), (4, [7, 0, 31, 16], False),
-                                               (2, [40, 9], True), (3, [5, 5, 5], True)])
+                                               (2, [40, 9], True), (3, [5, 5, 5], True),
+                                               (4, [512] * 4, False), (4, [512] * 4, True),
+                                               (3, [300, 0, 417], False)])
 def test_sharded_gather_rows_gloo(world, counts, skew):
-    """C5 sync-free exchange: ragged per-rank batches (one empty), ids skewed
-    onto one owner (the other windows own nothing): rows in batch order,
-    bit-exact (-0.0 and NaN payloads included); out-of-window ids counted."""
+    """C5 exchange: ragged per-rank batches (one empty), ids skewed onto one
+    owner (the other windows own nothing; at 4 x 512 positions that overflows
+    the owner segments and re-runs as the byte-MAX all-reduce): rows in batch
+    order, bit-exact (-0.0 and NaN payloads included); out-of-window ids
+    counted."""
     _run(world, _gather_worker, 997, 16, 3, counts, skew)
 
 
-def _scatter_worker(rank, world, n, d, b, seed):
+def _scatter_worker(rank, world, n, d, b, seed, skew=False):
     rng = np.random.default_rng(seed)
-    ids = rng.integers(0, n, size=b)
-    ids[: b // 4] = ids[0]                       # repeated ids accumulate
+    ids = rng.integers(0, shard_range(n, world, 0)[1] if skew else n, size=b)
+    ids[: b // 16] = ids[0]                      # repeated ids accumulate
     grads = [rng.standard_normal((b, d)).astype(np.float32) for _ in range(world)]  # every rank's contribution
     ref = np.zeros((n, d), np.float64)
     for g in grads:
@@ -220,6 +234,15 @@ def _scatter_worker(rank, world, n, d, b, seed):
                              scatter_add=scatter_add, status=status)
     np.testing.assert_allclose(shard_grad.numpy(), ref[rb:rb + rc], rtol=1e-5, atol=1e-5)
     assert status[0] == status[1] == b
+    cap = segment_capacity(b, world)
+    per_owner = np.bincount(owner_of(torch.from_numpy(ids), n, world).numpy(), minlength=world)
+    want = "all-reduce" if per_owner.max() > cap else "owner reduce-scatter"
+    assert sharded_mod.LAST_EXCHANGE["mode"] == want, (sharded_mod.LAST_EXCHANGE, cap)
+    for mode in ("allreduce", "segments"):
+        t = torch.zeros((rc, d))
+        sharded_scatter_add_rows(t, rb, torch.from_numpy(ids), torch.from_numpy(grads[rank]),
+                                 scatter_add=scatter_add, exchange=mode)
+        np.testing.assert_allclose(t.numpy(), ref[rb:rb + rc], rtol=1e-5, atol=1e-5)
     # an id outside every window is counted (sync-free) and raised with check=True
     bad = torch.from_numpy(ids).clone()
     bad[1] = n + 3
@@ -232,11 +255,12 @@ def _scatter_worker(rank, world, n, d, b, seed):
                                  scatter_add=scatter_add, check=True)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_scatter_add_rows_gloo(world):
+@pytest.mark.parametrize("world,b,skew", [(2, 64, False), (3, 64, False), (4, 2048, False), (4, 2048, True)])
+def test_sharded_scatter_add_rows_gloo(world, b, skew):
     """Trainable C5 table: row gradients of the global batch summed over ranks
-    (one all-reduce) and added by their owners into their shards."""
-    _run(world, _scatter_worker, 301, 8, 64, 13)
+    and added by their owners into their shards — by one reduce-scatter of
+    owner segments, or (a skewed batch overflowing a segment) one all-reduce."""
+    _run(world, _scatter_worker, 301, 8, b, 13, skew)
 
 
 def _dp_worker(rank, world):

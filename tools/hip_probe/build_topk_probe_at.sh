@@ -9,7 +9,9 @@ R=$(cd $H/../.. && pwd)
 PKG=real-time-recommendation-system-with-feature-store_amd
 T=$(mktemp -d /tmp/tkp.XXXX)
 mkdir -p $T/csrc $T/include
-if [ "$REV" = WORKTREE ]; then
+if [ -n "$SRCDIR" ]; then
+  cp $SRCDIR/$PKG/csrc/* $T/csrc/; cp $SRCDIR/include/* $T/include/
+elif [ "$REV" = WORKTREE ]; then
   cp $R/$PKG/csrc/* $T/csrc/; cp $R/include/* $T/include/
 else
   git -C $R archive $REV $PKG/csrc include | tar -x -C $T
