@@ -296,6 +296,37 @@ class FusedTrainStep:
             self.steps += warmup
         return g
 
+    def capture_body(self, body, extra_state=(), warmup: int = 2) -> torch.cuda.CUDAGraph:
+        """Capture ``body`` — a full step built from ``_grads`` and ``_update``
+        plus whatever device work the caller adds around it (e.g. the batch
+        source, ``FeederGraph``) — as ONE hipGraph. As in ``capture``, the
+        ``warmup`` eager runs are real steps, so the training state and
+        ``extra_state`` are snapshotted first and restored afterwards.
+        Single process only (a process group splits the step at its all-reduce)."""
+        if self.pg is not None:
+            raise RuntimeError("capture_body: data-parallel steps are captured as two graphs (capture())")
+        self.model.train()
+        tensors = self._state_tensors() + list(extra_state)
+        snap = [t.clone() for t in tensors]
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._ensure_clean()
+                body()
+                self._clean = True
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        with torch.no_grad():
+            for t, v in zip(tensors, snap):
+                t.copy_(v)
+        del snap
+        self._ensure_clean()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            body()
+        self._clean = True
+        return g
+
     def replay(self):
         self._ensure_clean()
         self.graph.replay()
@@ -306,3 +337,90 @@ class FusedTrainStep:
         self.steps += 1
         return self.loss_buf
 
+
+
+class FeederGraph:
+    """``DeviceFeeder`` batches and ``FusedTrainStep`` as ONE hipGraph per batch
+    — the reference's epoch loop (src/training/trainers/two_tower.py:84-156 over
+    the DataLoader of src/training/datasets/movielens.py:86-134) without a host
+    round trip per batch.
+
+    The epoch's permutation and a (batch cursor, sampler salt) pair live on the
+    device. One replay: the batch's interaction rows at the cursor (one
+    ``index_select`` of the permutation), their user / positive ids, the
+    on-device negatives (``rt_sample_negatives`` with the salt as its device
+    seed offset), the fused step, the loss into slot ``cursor`` of the epoch's
+    loss buffer, cursor and salt + 1. The batches are bit-identical to
+    iterating the feeder (same permutation generator, same sampler seeds), so
+    an epoch here equals the eager epoch step for step. A partial last batch
+    (``drop_last=False``) runs as an eager step."""
+
+    def __init__(self, step: FusedTrainStep, feeder):
+        if feeder.num_negatives <= 0:
+            raise ValueError("FeederGraph: the mixed-loss step needs negatives")
+        self.step, self.feeder = step, feeder
+        dev = step.dev
+        b, nn_ = feeder.batch_size, feeder.num_negatives
+        self.n_rows = int(feeder.inter_u.numel())
+        self.n_full = self.n_rows // b
+        self.order = torch.empty(self.n_rows, dtype=torch.int64, device=dev)
+        self.state = torch.zeros(2, dtype=torch.int64, device=dev)  # [batch cursor, sampler salt]
+        self.ar = torch.arange(b, dtype=torch.int64, device=dev)
+        self.pos_idx = torch.empty(b, dtype=torch.int64, device=dev)
+        self.rows = torch.empty(b, dtype=torch.int64, device=dev)
+        ids = torch.empty(b * (2 + nn_), dtype=torch.int64, device=dev)  # users | positives, negatives (adjacent)
+        self.users, self.pos, self.neg = ids[:b], ids[b:2 * b], ids[2 * b:]
+        self.losses = torch.zeros(max(1, len(feeder)), dtype=torch.float64, device=dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    def _body(self):
+        f, b = self.feeder, self.feeder.batch_size
+        torch.add(self.ar, self.state[0:1], alpha=b, out=self.pos_idx)
+        torch.index_select(self.order, 0, self.pos_idx, out=self.rows)
+        torch.index_select(f.inter_u, 0, self.rows, out=self.users)
+        torch.index_select(f.inter_m, 0, self.rows, out=self.pos)
+        kernels.sample_negatives(f.csr.offsets, f.csr.items, self.users, f.num_items, f.num_negatives,
+                                 seed=f.seed * 1_000_003, seed_offset=self.state[1:2],
+                                 out=self.neg.view(b, f.num_negatives))
+        self.step._grads(f.user_table, f.item_table, f.item_table, self.users, self.pos, self.neg)
+        loss = self.step._update()
+        self.losses.index_copy_(0, self.state[0:1], loss[0:1])
+        self.state.add_(1)
+
+    def _start_epoch(self, epoch: int):
+        f = self.feeder
+        if f.shuffle:
+            g = torch.Generator(device=self.step.dev)
+            g.manual_seed(f.seed + 7919 * epoch)  # the feeder's own permutation (DeviceFeeder.__iter__)
+            self.order.copy_(torch.randperm(self.n_rows, device=self.step.dev, generator=g))
+        else:
+            torch.arange(self.n_rows, out=self.order)
+        self.state.copy_(torch.tensor([0, epoch * 1_000_000], dtype=torch.int64))
+
+    def run_epoch(self, max_batches: int = 0) -> torch.Tensor:
+        """One epoch (at most ``max_batches`` batches when > 0) at the feeder's
+        epoch counter; returns the device fp64 per-batch losses."""
+        f = self.feeder
+        n_b = len(f)
+        if max_batches > 0:
+            n_b = min(n_b, max_batches)
+        n_graph = min(n_b, self.n_full)
+        epoch = f.epoch
+        if self.graph is None:  # warmup steps run on epoch 0's first batches, then everything is restored
+            self._start_epoch(epoch)
+            self.graph = self.step.capture_body(self._body, extra_state=(self.state, self.losses))
+        self._start_epoch(epoch)
+        self.step.model.train()
+        for _ in range(n_graph):
+            self.step._ensure_clean()
+            self.graph.replay()
+            self.step._clean = True
+        self.step.steps += n_graph
+        if n_b > n_graph:  # the partial last batch, eagerly (the feeder's own batch)
+            idx = self.order[n_graph * f.batch_size:]
+            bt = f.batch(idx, salt=epoch * 1_000_000 + n_graph)
+            loss = self.step(bt["user_table"], bt["item_table"], bt["item_table"], user_ids=bt["user_ids"],
+                             pos_ids=bt["pos_ids"], neg_ids=bt["neg_ids"])
+            self.losses[n_graph:n_graph + 1].copy_(loss[0:1])
+        f.epoch += 1
+        return self.losses[:n_b]

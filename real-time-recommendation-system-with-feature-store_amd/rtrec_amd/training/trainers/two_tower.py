@@ -73,6 +73,24 @@ class TwoTowerTrainer:
         self.val_losses: List[float] = []
 
     # ------------------------------------------------------------------
+    def _feeder_graph(self):
+        """(FeederGraph, batch limit) when the train loader is a ``DeviceFeeder``
+        (or an epoch-limited view of one: ``.feeder`` / ``.n``), the step is
+        single-process and ``config["graph_steps"]`` is not False; else None
+        (the eager loop over the loader's batches)."""
+        if not self.config.get("graph_steps", True) or self.step.pg is not None:
+            return None
+        from ..datasets.movielens import DeviceFeeder
+        from ..fused_step import FeederGraph
+        loader, limit = self.train_loader, 0
+        if not isinstance(loader, DeviceFeeder) and isinstance(getattr(loader, "feeder", None), DeviceFeeder):
+            loader, limit = loader.feeder, int(getattr(loader, "n", 0) or 0)
+        if not isinstance(loader, DeviceFeeder) or loader.num_negatives <= 0 or loader.batch_size % 32:
+            return None
+        if getattr(self, "_fg", None) is None or self._fg.feeder is not loader:
+            self._fg = FeederGraph(self.step, loader)
+        return self._fg, limit
+
     def _run_step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         dev = self.device
         if "user_ids" in batch:
@@ -89,6 +107,15 @@ class TwoTowerTrainer:
         fp64 slot per batch; the host reads them once at the end of the epoch
         (``last_epoch_step_losses``)."""
         self.model.train()
+        fg = self._feeder_graph()
+        if fg is not None:  # one hipGraph replay per batch (FeederGraph)
+            feeder, limit = fg
+            losses = feeder.run_epoch(limit)
+            self.last_epoch_step_losses = losses.cpu().numpy()
+            n = len(self.last_epoch_step_losses)
+            avg = float(self.last_epoch_step_losses.sum()) / n if n else 0.0
+            self.train_losses.append(avg)
+            return avg
         try:
             cap = len(self.train_loader)
         except TypeError:

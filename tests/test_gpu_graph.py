@@ -6,6 +6,7 @@ noise of the fp32/fp64 atomics that accumulate dW and the BN column sums).
 keeps them (``restore=False``)."""
 import copy
 
+import numpy as np
 import pytest
 import torch
 
@@ -132,3 +133,41 @@ def test_step_after_autograd_backward_matches_fresh_step(device):
     ref = s2(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone()
     got = s1(ut, mt, mt, user_ids=b[0], pos_ids=b[1], neg_ids=b[2]).clone()
     _check(m2, m1, [ref], [got])
+
+
+def test_feeder_graph_epoch_matches_eager(device):
+    """FeederGraph (batch rows at a device cursor, on-device negatives and the
+    fused step as one hipGraph per batch) reproduces the eager feeder-driven
+    loop: the same batches (ids compared exactly) and the same per-batch losses
+    (fp64 atomic reductions may reorder: 1e-5 relative), dropout on."""
+    from rtrec_amd.data.movielens import synthetic_movielens
+    from rtrec_amd.training.datasets.movielens import DeviceFeeder
+    from rtrec_amd.training.fused_step import FeederGraph, FusedTrainStep
+    from rtrec_amd.training.utils import create_two_tower_model_for_training
+    data = synthetic_movielens(seed=0)
+    torch.manual_seed(7)
+    cfg = {"embedding_dim": 64, "hidden_layers": [256, 128], "dropout_rate": 0.2, "temperature": 0.05}
+    m1 = create_two_tower_model_for_training(3, 20, cfg)
+    m2 = copy.deepcopy(m1)
+    m1.to(device)
+    m2.to(device)
+    mk = lambda: DeviceFeeder(data.train_interactions, data.users, data.movies, num_negatives=16,  # noqa: E731
+                              batch_size=256, device=device, seed=5)
+    fa, fb = mk(), mk()
+    sa, sb = FusedTrainStep(m1), FusedTrainStep(m2)
+    nb = 40
+    eager, last = [], None
+    for i, b in enumerate(fa):
+        if i == nb:
+            break
+        eager.append(float(sa(b["user_table"], b["item_table"], b["item_table"], user_ids=b["user_ids"],
+                              pos_ids=b["pos_ids"], neg_ids=b["neg_ids"])[0].item()))
+        last = b
+    fg = FeederGraph(sb, fb)
+    got = fg.run_epoch(max_batches=nb).cpu().numpy()
+    assert fb.epoch == 1
+    assert torch.equal(fg.users, last["user_ids"]) and torch.equal(fg.pos, last["pos_ids"])
+    assert torch.equal(fg.neg, last["neg_ids"])
+    np.testing.assert_allclose(got, np.asarray(eager), rtol=1e-5)
+    for (k, v1), v2 in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.allclose(v1.float(), v2.float(), rtol=1e-4, atol=1e-5), k
