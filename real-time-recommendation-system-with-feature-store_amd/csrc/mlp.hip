@@ -217,7 +217,7 @@ __device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, f
 // at the memory side where the slots live — and applies the running-stat
 // updates in segment order, with the same arithmetic as the consumer-side
 // finalisation below (linear_fwd_kernel, prev_final = 0).
-__device__ __noinline__ void bn_finalize_last(const rt_linear_fwd_args& a, unsigned nblk) {
+__device__ __forceinline__ void bn_finalize_last(const rt_linear_fwd_args& a, unsigned nblk) {
     __shared__ int last_s;
     const int tid = threadIdx.x, n = a.n;
     const bool two = a.seg_split > 0;

@@ -98,6 +98,8 @@ def flatip_topk(queries: torch.Tensor, items: torch.Tensor, k: int,
         raise TypeError("queries and items must share a dtype")
     if k <= 0:
         raise ValueError("k must be positive")
+    if k > TOPK_MAX_K:
+        return _flatip_topk_wide(queries, items, k, exclude_bits, id_offset, out)
     queries = queries.contiguous()
     items = items.contiguous()
     nq, d = queries.shape
@@ -122,6 +124,51 @@ def flatip_topk(queries: torch.Tensor, items: torch.Tensor, k: int,
                       bytes_=float((nq + nx) * d * queries.element_size() + nq * k * 12)):
         call("rt_flatip_topk", ptr(queries), nq, ptr(items) if nx else None, nx, d, dt, k, ptr(exclude_bits),
              words, id_offset, ptr(scores), ptr(ids), ptr(ws), ws.numel(), stream_of(queries))
+    return scores, ids
+
+
+TOPK_MAX_K = 512  # rt_flatip_topk: k <= 512 per launch (include/rtrec_hip.h)
+
+
+def _flatip_topk_wide(queries, items, k, exclude_bits, id_offset, out):
+    """k > 512 (faiss.IndexFlatIP.search takes any k, src/serving/retrieval.py:
+    170-171): ceil(k/512) exact passes of rt_flatip_topk, each excluding every
+    row the earlier passes returned (rt_exclusion_bitmap over their sorted ids,
+    OR-ed with the caller's bitmap). Each pass returns the best remaining rows
+    in (score desc, id asc) order, so the concatenation is the exact top-k in
+    that order; slots past the corpus are (-FLT_MAX, -1)."""
+    nq, nx = queries.shape[0], items.shape[0]
+    dev = queries.device
+    words = (nx + 31) // 32
+    if exclude_bits is not None:
+        exclude_bits = exclude_bits.contiguous()
+        if exclude_bits.dtype not in (torch.int32, torch.uint32) or exclude_bits.shape[0] != nq:
+            raise ValueError("exclude_bits must be int32/uint32 [nq, words]")
+        if exclude_bits.shape[1] < words:
+            raise ValueError("exclude_bits has fewer words than ceil(n_items / 32)")
+    parts_s, parts_i = [], []
+    found = None  # [nq, m] local row ids returned so far (-1 = none)
+    left = k
+    bits = exclude_bits
+    while left > 0:
+        kk = min(TOPK_MAX_K, left)
+        ps, pi = flatip_topk(queries, items, kk, exclude_bits=bits, id_offset=id_offset)
+        parts_s.append(ps)
+        parts_i.append(pi)
+        left -= kk
+        if left <= 0:
+            break
+        loc = torch.where(pi >= 0, pi - id_offset, torch.full_like(pi, -1))
+        found = loc if found is None else torch.cat([found, loc], dim=1)
+        srt = found.sort(dim=1).values.to(torch.int32).contiguous()
+        offs = torch.arange(nq + 1, dtype=torch.int64, device=dev) * srt.shape[1]
+        new = exclusion_bitmap_csr(offs, srt.reshape(-1), nx)
+        bits = new if exclude_bits is None else torch.bitwise_or(new, exclude_bits[:, :words].to(new.dtype))
+    scores, ids = torch.cat(parts_s, dim=1), torch.cat(parts_i, dim=1)
+    if out is not None:
+        out[0].copy_(scores)
+        out[1].copy_(ids)
+        return out
     return scores, ids
 
 

@@ -75,7 +75,8 @@ _STORAGE = {"float32": torch.float32, "float16": torch.float16, "bfloat16": torc
 
 
 MAX_DIM = 256   # rt_flatip_topk: d <= 256 (f32 d % 4 == 0, f16/bf16 d % 8 == 0)
-MAX_K = 512     # rt_flatip_topk / rt_topk_merge: k <= 512
+MAX_K_L2 = 512  # IndexFlatL2 mode: k <= 512 (its exact re-selection holds k_sel <= 512 candidates);
+                # the inner-product modes take any k (kernels.flatip_topk: k > 512 in exact 512-wide passes)
 
 
 def _default_device() -> torch.device:
@@ -188,10 +189,11 @@ class HipFlatIPIndex(IndexBase):
         distances (ascending, IndexFlatL2.search)."""
         if self.index is None:
             raise ValueError("Index not built yet")
-        if k > MAX_K:
-            raise ValueError(f"k={k} > {MAX_K}: the MI355X top-K kernels return at most {MAX_K} results per query")
         q = self._prepare(query_embeddings).to(self.storage_dtype)
         if self._l2:
+            if k > MAX_K_L2:
+                raise ValueError(f"k={k} > {MAX_K_L2}: the MI355X IndexFlatL2 mode returns at most {MAX_K_L2} "
+                                 "results per query (the inner-product metrics take any k)")
             return kernels.flatl2_topk(kernels.l2_augment(q, 0), self.index[: self.current_size], self.dimension, k,
                                        exclude_bits=exclude_bits)
         return kernels.flatip_topk(q, self.index[: self.current_size], k, exclude_bits=exclude_bits)

@@ -139,14 +139,17 @@ def test_feeder_graph_epoch_matches_eager(device):
     """FeederGraph (batch rows at a device cursor, on-device negatives and the
     fused step as one hipGraph per batch) reproduces the eager feeder-driven
     loop: the same batches (ids compared exactly) and the same per-batch losses
-    (fp64 atomic reductions may reorder: 1e-5 relative), dropout on."""
+    (fp64 atomic reductions may reorder: 1e-5 relative). Dropout off: a
+    captured step draws its masks from the device counter with seeds fixed at
+    capture, an eager step from fresh host seeds (the mask contract itself is
+    tests/test_gpu_dropout.py)."""
     from rtrec_amd.data.movielens import synthetic_movielens
     from rtrec_amd.training.datasets.movielens import DeviceFeeder
     from rtrec_amd.training.fused_step import FeederGraph, FusedTrainStep
     from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = synthetic_movielens(seed=0)
     torch.manual_seed(7)
-    cfg = {"embedding_dim": 64, "hidden_layers": [256, 128], "dropout_rate": 0.2, "temperature": 0.05}
+    cfg = {"embedding_dim": 64, "hidden_layers": [256, 128], "dropout_rate": 0.0, "temperature": 0.05}
     m1 = create_two_tower_model_for_training(3, 20, cfg)
     m2 = copy.deepcopy(m1)
     m1.to(device)

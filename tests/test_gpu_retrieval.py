@@ -175,12 +175,61 @@ def test_flatip_errors(K):
     from rtrec_amd.native import RTError
     with pytest.raises(RTError):  # fp32 rows must be 16-byte multiples (d % 4 == 0)
         K.flatip_topk(torch.randn(4, 10).cuda(), torch.randn(10, 10).cuda(), 5)
-    with pytest.raises(RTError):  # k above the supported maximum
-        K.flatip_topk(torch.randn(4, 16).cuda(), torch.randn(10, 16).cuda(), 4096)
     with pytest.raises(ValueError):
         K.flatip_topk(torch.randn(4, 16).cuda(), torch.randn(10, 32).cuda(), 5)
     with pytest.raises(RuntimeError):
         K.flatip_topk(torch.randn(4, 16), torch.randn(10, 16), 5)  # CPU tensors: no fallback
+
+
+@pytest.mark.parametrize("nq,nx,d,k,dtype", [(64, 3000, 128, 1100, torch.float32), (20, 600, 64, 700, torch.float32),
+                                             (33, 2500, 128, 513, torch.float16), (40, 9000, 96, 1024, torch.bfloat16)])
+def test_flatip_wide_k_vs_oracle(K, nq, nx, d, k, dtype):
+    """k > 512 (Faiss takes any k, src/serving/retrieval.py:170-171): exact
+    512-wide passes, each excluding the rows the earlier ones returned —
+    bit-exact against the oracle (fp32 on random data, 16-bit on dyadic
+    data), k > N padded, with an exclusion bitmap and an id offset."""
+    rng = np.random.default_rng(nq + nx + k)
+    if dtype == torch.float32:
+        q = rng.standard_normal((nq, d)).astype(np.float32)
+        x = rng.standard_normal((nx, d)).astype(np.float32)
+    else:
+        q = (rng.integers(-64, 65, size=(nq, d)) / 64.0).astype(np.float32)
+        x = (rng.integers(-64, 65, size=(nx, d)) / 64.0).astype(np.float32)
+    excl = [rng.choice(nx, int(rng.integers(0, nx // 3)), replace=False) for _ in range(nq)]
+    bm_np = orc.exclusion_bitmap(nq, nx, excl)
+    bm = K.exclusion_bitmap(nq, nx, excl, "cuda")
+    for bits, bits_np, off in ((None, None, 0), (bm, bm_np, 777)):
+        rs, ri = orc.flat_ip_search(q, x, k, exclude_bits=bits_np, id_offset=off, nthreads=8)
+        gs, gi = K.flatip_topk(torch.from_numpy(q).to(dtype).cuda(), torch.from_numpy(x).to(dtype).cuda(), k,
+                               exclude_bits=bits, id_offset=off)
+        assert np.array_equal(gi.cpu().numpy(), ri)
+        assert np.array_equal(gs.cpu().numpy(), rs)
+
+
+def test_index_search_wide_k_and_filter(K):
+    """HipFlatIPIndex.search with k > 512 and with filter_ids at k = 300
+    (k_search = 600 > 512), as faiss-backed FaissIndex.search allows."""
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex
+    rng = np.random.default_rng(12)
+    emb = rng.standard_normal((2000, 64)).astype(np.float32)
+    ids = [f"m{i}" for i in range(2000)]
+    idx = HipFlatIPIndex({"dimension": 64})
+    idx.build(emb, ids)
+    q = rng.standard_normal((3, 64)).astype(np.float32)
+    got, sc = idx.search(q, 900)
+    e, qn = emb.copy(), q.copy()
+    orc.normalize_L2(e)  # faiss.normalize_L2, bit-exact with the index's rt_l2_renorm_f32
+    orc.normalize_L2(qn)
+    rs, ri = orc.flat_ip_search(qn, e, 900, nthreads=4)
+    assert [len(g) for g in got] == [900, 900, 900]
+    for row, want in zip(got, ri):
+        assert row == [ids[j] for j in want]
+    allowed = ids[::3]
+    fgot, _ = idx.search(q, 300, filter_ids=allowed)
+    aset = set(allowed)
+    for row, want in zip(fgot, ri):
+        exp = [ids[j] for j in want[:600] if ids[j] in aset][:300]
+        assert row == exp
 
 
 def test_topk_merge(K):
