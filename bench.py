@@ -277,9 +277,11 @@ def topk_extras(dev):
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
     tf = s["flops"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e12
+    tb, tsrc = pmc_traffic("flatip_topk_c4")
     out["topk_c4_shard"] = {"qps": 65536 / el, "ms": el * 1e3, "kernel_ms": s["avg_ms"], "tflops": tf,
                             "mfma_frac": tf / PEAK_BF16_TFLOPS, "dtype": "f16", "k": 100,
-                            "shape": "65536x125000x128"}
+                            "shape": "65536x125000x128", "compulsory_bytes": 2 * (65536 + 125000) * 128 + 65536 * 100 * 12,
+                            "traffic_per_call": tb, "traffic_source": tsrc}
     del q, x
     # config 5 gather: bf16 rows of 256 from a 12.5M-row shard, 16M ids per launch
     rows = 12_500_000
@@ -295,8 +297,10 @@ def topk_extras(dev):
     s = TIMER.summary()["gather_rows"]
     TIMER.disable()
     gbs = s["bytes"] / s["count"] / (s["avg_ms"] * 1e-3) / 1e9
+    tb, tsrc = pmc_traffic("gather_c5")
     out["gather_c5"] = {"GBps": gbs, "hbm_frac": gbs / PEAK_HBM_GBS, "ms": s["avg_ms"], "ids": ids.numel(),
-                        "row_bytes": 512}
+                        "row_bytes": 512, "algorithmic_bytes": 2 * 512 * ids.numel() + 8 * ids.numel(),
+                        "traffic": tb, "traffic_source": tsrc}
     del table, ids, outb
     torch.cuda.empty_cache()
     # config 5 in-batch scoring: S = U·Pᵀ/τ over B=8192 users x 8192 items, D=256
@@ -397,7 +401,7 @@ PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA, MI355X_MICROARCH.md
 KERNEL_SOURCES = {
     "linear_fwd": ["mlp.hip", "split3.h", "rt_common.h"], "linear_bwd_dz": ["mlp.hip", "split3.h", "rt_common.h"],
     "linear_bwd_dw": ["mlp.hip", "split3.h", "rt_common.h"], "loss_fwd_bwd": ["loss.hip", "split3.h", "rt_common.h"],
-    "clip_adam": ["optim.hip", "rt_common.h"],
+    "clip_adam": ["optim.hip", "rt_common.h"], "gather_c5": ["gather.hip", "rt_common.h"],
     "flatip_topk_c4": ["topk_api.hip", "topk_f16.hip", "topk_impl.h", "topk_v1.h", "topk_v2.h", "topk_v3.h",
                        "topk_v4.h", "topk_dense.h", "rt_sort.h", "rt_common.h"],
 }

@@ -210,6 +210,18 @@ __device__ __forceinline__ void bn_affine(float gamma, float beta, float mean, f
     shift = __builtin_fmaf(-mean, scale, beta);
 }
 
+// Before a last-block ticket: this thread's slot atomics are performed. Every
+// value the last block reads was written by device-scope atomics and is read
+// back by returning atomics, so no cache writeback is needed — an agent-scope
+// release fence here is a buffer_wbl2 (a write-back of the XCD's L2) in every
+// block (-DRT_TICKET_WBL2 restores it for A/B builds).
+__device__ __forceinline__ void ticket_release() {
+#ifdef RT_TICKET_WBL2
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // BatchNorm finalisation by the producing forward launch (rt_linear_fwd_args
 // fin_*): every block calls this after its stats atomics; the group's last
 // block (ticket counter past the slots) derives the batch mean / invstd of
@@ -225,8 +237,7 @@ __device__ __forceinline__ void bn_finalize_last(const rt_linear_fwd_args& a, un
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slot atomics are performed
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ticket_release();
         unsigned long long* cnt =
             reinterpret_cast<unsigned long long*>(a.stats_out + static_cast<int64_t>(nseg) * RT_STAT_SLOTS * 2 * n);
         last_s = atomicAdd(cnt, 1ull) == static_cast<unsigned long long>(nblk) - 1ull ? 1 : 0;
@@ -1527,8 +1538,7 @@ __global__ __launch_bounds__(DW_NT) void linear_bwd_dw_kernel(BwdLaunch L) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's slot atomics are performed
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            ticket_release();
             unsigned long long* cnt = reinterpret_cast<unsigned long long*>(a.dbias_slots + static_cast<int64_t>(RT_STAT_SLOTS) * n);
             const unsigned long long nsplit = static_cast<unsigned long long>((m + rows_per_split - 1) / rows_per_split);
             last_s = atomicAdd(&cnt[bx], 1ull) == nsplit - 1 ? 1 : 0;

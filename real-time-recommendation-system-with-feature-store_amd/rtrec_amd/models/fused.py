@@ -218,8 +218,12 @@ STAT_SLOTS = 16
 # launch's per-tile tickets, so a region of STAT_SLOTS + 1 rows covers every variant
 DBIAS_ROWS = STAT_SLOTS + 1
 # BatchNorm batch statistics finalised once by the producing forward launch
-# (rt_linear_fwd_args.fin_*) instead of by every block of the consuming launch
-FINALIZE_BN_IN_PRODUCER = os.environ.get("RTREC_BN_FINAL", "1") != "0"
+# (rt_linear_fwd_args.fin_*: its last block, found by a ticket) instead of by
+# every block of the consuming launch. Off by default: the consumer's slot
+# reads overlap its A-tile loads, while the producer's ticket and serial tail
+# cost more — C2 step 0.2392 -> 0.2505 ms in a same-box A/B
+# (profiles/r05_c2_ab_bn_final.txt). RTREC_BN_FINAL=1 turns it on.
+FINALIZE_BN_IN_PRODUCER = os.environ.get("RTREC_BN_FINAL", "0") == "1"
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:

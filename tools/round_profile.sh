@@ -25,5 +25,9 @@ python3 $R/tools/pmc_dump.py $(find $P/f $P/w -name "*.db") --filter rt:: > $O/c
 python3 $R/tools/prof_topk.py 100 3 > /dev/null
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $P/tf -o tf -- python3 $R/tools/prof_topk.py 100 2 > $P/tf.log 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $P/tw -o tw -- python3 $R/tools/prof_topk.py 100 2 > $P/tw.log 2>&1 || exit 1
-python3 $R/tools/pmc_dump.py $(find $P/tf $P/tw -name "*.db") --filter topk > $O/topk_c4_traffic_pmc.txt
+python3 $R/tools/pmc_dump.py $(find $P/tf $P/tw -name "*.db") --filter topk --calls 2 > $O/topk_c4_traffic_pmc.txt
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $P/gf -o gf -- python3 $R/tools/prof_gather.py 2 > $P/gf.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $P/gw -o gw -- python3 $R/tools/prof_gather.py 2 > $P/gw.log 2>&1 || exit 1
+python3 $R/tools/pmc_dump.py $(find $P/gf $P/gw -name "*.db") --filter gather > $O/gather_c5_traffic_pmc.txt
+TOPK_CALLS=2 python3 $R/tools/traffic_json.py $O/c2_traffic_pmc.txt $O/topk_c4_traffic_pmc.txt $O/gather_c5_traffic_pmc.txt > $O/traffic.json || true
 ls -la $O

@@ -30,7 +30,8 @@ FAMILY = {"linear_fwd_kernel": ["linear_fwd"], "linear_bwd_dz_kernel": ["linear_
           "linear_bwd_dw_kernel": ["linear_bwd_dw"], "loss_fwd_kernel": ["loss_fwd_bwd"],
           "loss_bwd_kernel": ["loss_fwd_bwd"], "clip_adam_kernel": ["clip_adam"],
           "grad_sqnorm_kernel": ["clip_adam"], "flatip_topk_v2_kernel": ["flatip_topk_c4"],
-          "flatip_topk_v4_scan": ["flatip_topk_c4"], "flatip_topk_v4_finish": ["flatip_topk_c4"]}
+          "flatip_topk_v4_scan": ["flatip_topk_c4"], "flatip_topk_v4_finish": ["flatip_topk_c4"],
+          "gather_rows_kernel": ["gather_c5"]}
 
 
 def parse(path):
@@ -70,7 +71,8 @@ for (name, fam), b in tot.items():
     launches = max(disp[(k, f)] for (k, f) in disp if k == name)
     per[name] += b / launches
 json.dump({"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes: "
-                     "bench.py --steps 10 --warmup 3 --no-extras --no-cpu-baseline and tools/prof_topk.py 100 2",
+                     "bench.py --steps 10 --warmup 3 --no-extras --no-cpu-baseline, tools/prof_topk.py 100 2 and "
+                     "tools/prof_gather.py 2",
            "correction": "bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE halves wide 16-B/lane reads)",
            "kernel_sources_sha": {k: _bench_module()._kernel_sources_sha(k) for k in per},
            "bytes_per_launch": {k: round(v) for k, v in per.items()},
