@@ -145,6 +145,18 @@ int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* pos_items, in
                         const int64_t* users, int64_t n, int64_t num_items, int num_neg, uint64_t seed,
                         const uint64_t* seed_offset, int64_t* out, void* stream);
 
+/* Device batch cursor of a graph-captured epoch (rtrec_amd FeederGraph; the
+ * DataLoader batches of src/training/datasets/movielens.py:86-134 over a
+ * shuffled interaction list). state = int64 [2] device {batch cursor b,
+ * sampler salt}. rt_feeder_batch: row t < batch of batch b is interaction
+ * order[b·batch + t]: users[t] = inter_u[row], pos[t] = inter_m[row]
+ * (order holds >= (b+1)·batch entries). rt_feeder_commit (one thread, after
+ * the step): losses[b] = loss[0], then b += 1 and salt += 1 (the salt is the
+ * seed_offset of the batch's rt_sample_negatives). */
+int rt_feeder_batch(const int64_t* order, const int64_t* inter_u, const int64_t* inter_m, const int64_t* state,
+                    int64_t batch, int64_t* users, int64_t* pos, void* stream);
+int rt_feeder_commit(const double* loss, double* losses, int64_t n_losses, int64_t* state, void* stream);
+
 /* ------------------------------------------------------------------------
  * Tower MLP (src/models/two_tower.py:56-72,98-134,196-212,238-281):
  * hidden block l = Linear → act → BatchNorm1d → Dropout, final Linear, then

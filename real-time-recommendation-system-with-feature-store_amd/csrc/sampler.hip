@@ -161,6 +161,29 @@ __global__ __launch_bounds__(256) void sample_negatives_kernel(const int64_t* __
     if (active) o[lane] = mine;  // -1 only if kMaxRounds ran out (pool > num_neg makes that vanishing)
 }
 
+// graph-captured epoch: the batch at the device cursor (rt_feeder_batch) and
+// the post-step bookkeeping (rt_feeder_commit)
+__global__ __launch_bounds__(256) void feeder_batch_kernel(const int64_t* __restrict__ order,
+                                                           const int64_t* __restrict__ inter_u,
+                                                           const int64_t* __restrict__ inter_m,
+                                                           const int64_t* __restrict__ state, int64_t batch,
+                                                           int64_t* __restrict__ users, int64_t* __restrict__ pos) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= batch) return;
+    const int64_t row = order[state[0] * batch + t];
+    users[t] = inter_u[row];
+    pos[t] = inter_m[row];
+}
+
+__global__ void feeder_commit_kernel(const double* __restrict__ loss, double* __restrict__ losses, int64_t n_losses,
+                                     int64_t* __restrict__ state) {
+    if (threadIdx.x != 0) return;
+    const int64_t b = state[0];
+    if (b >= 0 && b < n_losses) losses[b] = loss[0];
+    state[0] = b + 1;
+    state[1] += 1;
+}
+
 }  // namespace sampler
 }  // namespace rt
 
@@ -183,4 +206,20 @@ extern "C" int rt_sample_negatives(const int64_t* pos_offsets, const int32_t* po
                            pos_offsets, pos_items, n_users, users, n, num_items, num_neg, seed, seed_offset, out);
     }
     return check_launch("sample_negatives_kernel");
+}
+
+extern "C" int rt_feeder_batch(const int64_t* order, const int64_t* inter_u, const int64_t* inter_m,
+                               const int64_t* state, int64_t batch, int64_t* users, int64_t* pos, void* stream) {
+    if (batch < 0 || (batch > 0 && (!order || !inter_u || !inter_m || !state || !users || !pos))) return RT_ERR_INVALID;
+    if (batch == 0) return RT_OK;
+    hipLaunchKernelGGL(sampler::feeder_batch_kernel, dim3(static_cast<unsigned>((batch + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), order, inter_u, inter_m, state, batch, users, pos);
+    return check_launch("feeder_batch_kernel");
+}
+
+extern "C" int rt_feeder_commit(const double* loss, double* losses, int64_t n_losses, int64_t* state, void* stream) {
+    if (!loss || !losses || !state || n_losses < 0) return RT_ERR_INVALID;
+    hipLaunchKernelGGL(sampler::feeder_commit_kernel, dim3(1), dim3(64), 0, as_stream(stream), loss, losses, n_losses,
+                       state);
+    return check_launch("feeder_commit_kernel");
 }

@@ -85,6 +85,8 @@ SIGNATURES = {
     "rt_topk_merge": (c_int, [vp, vp, c_i64, c_int, c_int, c_int, vp, vp, vp]),
     "rt_flatip_topk_tuning": (c_int, [c_int, c_int, c_int]),
     "rt_sample_negatives": (c_int, [vp, vp, c_i64, vp, c_i64, c_i64, c_int, c_u64, vp, vp, vp]),
+    "rt_feeder_batch": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp]),
+    "rt_feeder_commit": (c_int, [vp, vp, c_i64, vp, vp]),
     "rt_linear_fwd_f32": (c_int, [ctypes.POINTER(LinearFwdArgs), vp]),
     "rt_linear_bwd_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),
     "rt_linear_bwd_dz_f32": (c_int, [ctypes.POINTER(LinearBwdArgs), vp]),

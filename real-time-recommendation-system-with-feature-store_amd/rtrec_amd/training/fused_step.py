@@ -346,11 +346,11 @@ class FeederGraph:
     round trip per batch.
 
     The epoch's permutation and a (batch cursor, sampler salt) pair live on the
-    device. One replay: the batch's interaction rows at the cursor (one
-    ``index_select`` of the permutation), their user / positive ids, the
-    on-device negatives (``rt_sample_negatives`` with the salt as its device
-    seed offset), the fused step, the loss into slot ``cursor`` of the epoch's
-    loss buffer, cursor and salt + 1. The batches are bit-identical to
+    device. One replay: the batch's user / positive ids at the cursor
+    (``rt_feeder_batch``), the on-device negatives (``rt_sample_negatives``
+    with the salt as its device seed offset), the fused step, then
+    ``rt_feeder_commit``: the loss into slot ``cursor`` of the epoch's loss
+    buffer, cursor and salt + 1. The batches are bit-identical to
     iterating the feeder (same permutation generator, same sampler seeds), so
     an epoch here equals the eager epoch step for step. A partial last batch
     (``drop_last=False``) runs as an eager step."""
@@ -365,9 +365,6 @@ class FeederGraph:
         self.n_full = self.n_rows // b
         self.order = torch.empty(self.n_rows, dtype=torch.int64, device=dev)
         self.state = torch.zeros(2, dtype=torch.int64, device=dev)  # [batch cursor, sampler salt]
-        self.ar = torch.arange(b, dtype=torch.int64, device=dev)
-        self.pos_idx = torch.empty(b, dtype=torch.int64, device=dev)
-        self.rows = torch.empty(b, dtype=torch.int64, device=dev)
         ids = torch.empty(b * (2 + nn_), dtype=torch.int64, device=dev)  # users | positives, negatives (adjacent)
         self.users, self.pos, self.neg = ids[:b], ids[b:2 * b], ids[2 * b:]
         self.losses = torch.zeros(max(1, len(feeder)), dtype=torch.float64, device=dev)
@@ -375,17 +372,15 @@ class FeederGraph:
 
     def _body(self):
         f, b = self.feeder, self.feeder.batch_size
-        torch.add(self.ar, self.state[0:1], alpha=b, out=self.pos_idx)
-        torch.index_select(self.order, 0, self.pos_idx, out=self.rows)
-        torch.index_select(f.inter_u, 0, self.rows, out=self.users)
-        torch.index_select(f.inter_m, 0, self.rows, out=self.pos)
+        st = native.stream_of(self.order)
+        call("rt_feeder_batch", ptr(self.order), ptr(f.inter_u), ptr(f.inter_m), ptr(self.state), b,
+             ptr(self.users), ptr(self.pos), st)
         kernels.sample_negatives(f.csr.offsets, f.csr.items, self.users, f.num_items, f.num_negatives,
                                  seed=f.seed * 1_000_003, seed_offset=self.state[1:2],
                                  out=self.neg.view(b, f.num_negatives))
         self.step._grads(f.user_table, f.item_table, f.item_table, self.users, self.pos, self.neg)
         loss = self.step._update()
-        self.losses.index_copy_(0, self.state[0:1], loss[0:1])
-        self.state.add_(1)
+        call("rt_feeder_commit", ptr(loss), ptr(self.losses), self.losses.numel(), ptr(self.state), st)
 
     def _start_epoch(self, epoch: int):
         f = self.feeder
