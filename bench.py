@@ -444,7 +444,7 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
     (rtrec_amd/dist/sharded.py::sharded_topk_owner). Strong scaling (fixed corpus);
     time = max over ranks between barriers."""
     from rtrec_amd import kernels
-    from rtrec_amd.dist.sharded import shard_range, sharded_topk_owner
+    from rtrec_amd.dist.sharded import LAST_TOPK, ShardOps, shard_range, sharded_topk_global
     n, d, nq, k = 1_000_000, 128, 65536, 100
     b, c = shard_range(n, world, rank)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -453,9 +453,10 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
     q = torch.nn.functional.normalize(torch.randn(nq, d, device=dev, generator=gq), dim=1).half()
     grp = dist.group.WORLD if dist is not None else None
 
-    def run():
-        return sharded_topk_owner(q, k, lambda qq, kk: kernels.flatip_topk(qq, shard, kk, id_offset=b),
-                                  kernels.topk_merge, grp)
+    ops = ShardOps(shard, b)
+
+    def run():  # N > 1: one corpus-wide threshold per query (N = 1: the plain single-GPU search)
+        return sharded_topk_global(q, k, n, ops, kernels.topk_merge, grp, owner=True)
 
     def sync():
         torch.cuda.synchronize()
@@ -477,8 +478,71 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
     del shard, q
     torch.cuda.empty_cache()
     return {"qps": nq * reps / el, "ms_per_launch": 1e3 * el / reps, "n_gpus": world, "corpus_rows": n,
-            "shard_rows": c, "queries_per_launch": nq, "k": k, "dtype": "f16", "exchange": "all_to_all + owner merge",
+            "shard_rows": c, "queries_per_launch": nq, "k": k, "dtype": "f16",
+            "exchange": ("sample lists all-gather + stage-count all-reduce, shard search against one corpus-wide "
+                         "threshold per query, all_to_all + owner merge" if world > 1 else "none (N = 1)"),
+            "global_threshold": dict(LAST_TOPK) if world > 1 else None,
             "scaling": "strong (fixed 1M-row corpus)"}
+
+
+def topk_c4_n8_emulated(dev, reps=3):
+    """The per-rank work of the C4 1M-corpus search at N = 8, run on this one
+    GPU (collectives excluded): (a) replicated corpus, 8,192 of the 65,536
+    queries; (b) row shard 0 of 8 (125,000 rows) searched against one
+    corpus-wide threshold per query — its sample, the threshold from the 8
+    shards' sample lists (the other 7 precomputed, as the all-gather would
+    deliver them), the shard search; (c) the same shard with its own
+    threshold (the plain sharded search). Speed-up = the one-GPU 1M call over
+    each per-rank time."""
+    from rtrec_amd import kernels
+    from rtrec_amd.dist.sharded import shard_range
+    n, d, nq, k, world = 1_000_000, 128, 65536, 100, 8
+    g = torch.Generator(device=dev).manual_seed(1000)
+    corpus = torch.nn.functional.normalize(torch.randn(n, d, device=dev, generator=g), dim=1).half()
+    gq = torch.Generator(device=dev).manual_seed(99)
+    q = torch.nn.functional.normalize(torch.randn(nq, d, device=dev, generator=gq), dim=1).half()
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return 1e3 * (time.perf_counter() - t0) / reps
+    t_full = timed(lambda: kernels.flatip_topk(q, corpus, k))
+    mine = q[:nq // world].contiguous()
+    t_repl = timed(lambda: kernels.flatip_topk(mine, corpus, k))
+    b0, c0 = shard_range(n, world, 0)
+    shard0 = corpus[b0:b0 + c0]
+    stride = kernels.shard_sample_stride(n)
+    lists, sampled, stages = [], 0, 0
+    for r in range(world):
+        b, c = shard_range(n, world, r)
+        top, (sa, st) = kernels.flatip_topk_shard_sample(q, corpus[b:b + c], k, stride)
+        lists.append(top)
+        sampled += sa
+        stages += st
+    rank = kernels.topk_sample_rank(k, sampled, stages)
+    stacked = torch.stack(lists)
+
+    def rank_work():
+        kernels.flatip_topk_shard_sample(q, shard0, k, stride)
+        thr = kernels.topk_sample_threshold(stacked, rank)
+        return kernels.flatip_topk_shard_search(q, shard0, k, thr, id_offset=b0)
+    t_glob = timed(rank_work)
+    _, ids = rank_work()
+    cands = float((ids >= 0).sum(dim=1).float().mean())
+    t_plain = timed(lambda: kernels.flatip_topk(q, shard0, k, id_offset=b0))
+    del corpus, q, mine, stacked, lists
+    torch.cuda.empty_cache()
+    return {"one_gpu_1m_ms": t_full,
+            "replicated_rank_ms": t_repl, "replicated_speedup": t_full / t_repl,
+            "global_threshold_rank_ms": t_glob, "global_threshold_speedup": t_full / t_glob,
+            "global_threshold_candidates_per_query": cands, "sample_rank": rank, "sample_stride": stride,
+            "shard_local_threshold_rank_ms": t_plain, "shard_local_speedup": t_full / t_plain,
+            "note": "per-rank device time at N = 8 on one GPU, collectives excluded (the driver's 8-GPU SCALE "
+                    "run measures them)"}
 
 
 def topk_c4_replicated(dev, dist, rank, world, reps=3):
@@ -735,7 +799,10 @@ def main():
                 result["extras"] = topk_extras(dev)
             except Exception as e:  # extras never hide the headline
                 result["extras"] = {"error": repr(e)}
-            for name, fn in (("c2_with_feeder", lambda: c2_with_feeder(dev)), ("c1_train_epoch", lambda: c1_epoch(dev))):
+            legs = [("c2_with_feeder", lambda: c2_with_feeder(dev)), ("c1_train_epoch", lambda: c1_epoch(dev))]
+            if world == 1:
+                legs.append(("topk_c4_n8_emulated", lambda: topk_c4_n8_emulated(dev)))
+            for name, fn in legs:
                 try:
                     result["extras"][name] = fn()
                 except Exception as e:

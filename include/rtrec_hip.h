@@ -92,13 +92,52 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
                    float* out_scores, int64_t* out_ids, void* workspace, size_t workspace_bytes,
                    void* stream);
 
+/* Corpus-sharded search with ONE corpus-wide threshold per query (several
+ * GPUs, each holding a row shard of the corpus that faiss.IndexFlatIP.search
+ * would scan whole, src/serving/retrieval.py:141-197): every rank samples its
+ * shard, the ranks' samples give each query a threshold that is, w.h.p., at
+ * most its k-th score over the WHOLE corpus, and each rank keeps only its
+ * rows at or above it — so a query's candidates per shard shrink with the
+ * number of shards instead of staying ~k per shard.
+ *   rt_flatip_topk_shard_sample: top32 [nq][32] = per query the 32 largest
+ *     group maxima (max of 16 rows) over every stride-th 128-row stage of the
+ *     shard, sorted descending (-inf padded); stage_counts = {sampled stages,
+ *     stages} of this shard.
+ *   rt_topk_sample_rank: the failure-safe rank (P(threshold > k-th) < 1e-6)
+ *     for the sampled fraction sum(sampled) / sum(stages) over all shards
+ *     (0 = none fits: search from -inf).
+ *   rt_topk_sample_threshold: thr[q] = the rank-th largest of the union of
+ *     n_lists such lists (layout [n_lists][nq][32], e.g. all-gathered over
+ *     ranks); -FLT_MAX when the union has fewer finite entries.
+ *   rt_flatip_topk_shard_search: this shard's rows with score >= thr[q], the
+ *     best k of them per query in (score desc, id asc) order, padded with
+ *     (-FLT_MAX, -1) when fewer pass. The caller merges the shards' lists;
+ *     a query whose merged list holds < min(k, corpus rows) entries had a
+ *     threshold above its k-th and is searched again from -inf.
+ * f16/bf16 with d % 8 == 0, d <= 128, k <= 128, one query chunk (the v4
+ * kernel plan of rt_flatip_topk); RT_ERR_UNSUPPORTED otherwise. The
+ * workspace (rt_flatip_topk_shard_workspace_bytes, 0 = unsupported) serves
+ * both the sample and the search of the same shape. */
+size_t rt_flatip_topk_shard_workspace_bytes(int64_t nq, int64_t nx, int d, int dtype, int k);
+int rt_flatip_topk_shard_sample(const void* queries, int64_t nq, const void* items, int64_t nx, int d, int dtype,
+                                int k, int stride, float* top32, int64_t* stage_counts, void* workspace,
+                                size_t workspace_bytes, void* stream);
+int rt_topk_sample_rank(int k, int64_t sampled_stages, int64_t stages, int* rank);
+int rt_topk_sample_threshold(const float* lists, int n_lists, int64_t nq, int rank, float* thr, void* stream);
+int rt_flatip_topk_shard_search(const void* queries, int64_t nq, const void* items, int64_t nx, int d, int dtype,
+                                int k, const float* thr, int64_t id_offset, float* out_scores, int64_t* out_ids,
+                                void* workspace, size_t workspace_bytes, void* stream);
+
 /* Planner override of rt_flatip_topk (tests and tuning; process-wide, not
  * thread-safe, results unchanged by any setting). v4_mode: 0 automatic, 1 never
  * the sampled-threshold kernel pair, 2 it wherever legal (16-bit, d <= 128,
  * k <= 128); + 4: per-split thresholds instead of one corpus-wide threshold
  * per query when the items are split; + 8: fp32 corpora of <= 4096 rows keep
  * the fused register-list scan instead of the score-slab GEMM + per-query
- * select pair (the default for them). v4_stride: sample every stride-th 128-row stage (0 = planner).
+ * select pair (the default for them); + 16: a corpus-wide threshold is
+ * sampled by every block over the whole corpus (the round-4 form) instead of
+ * by one sample-only launch over every split and a per-query threshold pass.
+ * v4_stride: sample every stride-th 128-row stage (0 = planner).
  * v4_rank: threshold = rank-th largest sampled group maximum (-1 = planner,
  * 0 = no sample: a running threshold from -inf). Set before sizing the
  * workspace. */

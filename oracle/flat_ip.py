@@ -145,3 +145,46 @@ def dot_fma(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Sequential fmaf-chain dot products of rows (float64 emulation is exact for
     dyadic inputs only; general bit-exact scores come from flatip.c)."""
     return (a.astype(np.float64) @ b.astype(np.float64).T).astype(np.float32)
+
+
+def sample_rank(k: int, sampled: int, stages: int) -> int:
+    """Restatement of rt_topk_sample_rank (csrc/topk_api.hip): the smallest
+    rank r <= 32 with P(Bin(k, f) >= r) <= 1e-6 for f = sampled / stages
+    (0 when none), the failure bound of a threshold taken as the r-th largest
+    sampled group maximum."""
+    import math
+    f = sampled / stages
+
+    def log_tail(r):
+        if r > k:
+            return -1e300
+        terms = [math.lgamma(k + 1) - math.lgamma(i + 1) - math.lgamma(k - i + 1) + i * math.log(f) +
+                 ((k - i) * math.log1p(-f) if f < 1 else (0.0 if i == k else -1e300)) for i in range(r, k + 1)]
+        mx = max(terms)
+        return mx + math.log(sum(math.exp(t - mx) for t in terms))
+    for r in range(1, 33):
+        if log_tail(r) <= math.log(1e-6):
+            return r
+    return 0
+
+
+def shard_sample(queries: np.ndarray, shard: np.ndarray, stride: int, nt: int = 128, group: int = 16):
+    """CPU stand-in of rt_flatip_topk_shard_sample for the orchestration tests:
+    per query the 32 largest maxima of 16-row groups over every stride-th
+    nt-row stage of the shard (exact float64 scores of dyadic data), -inf
+    padded, and the (sampled, total) stage counts. Any grouping gives the
+    same failure bound (a group maximum above the k-th score needs a top-k
+    row in the group)."""
+    n = shard.shape[0]
+    stages = -(-n // nt)
+    rows = np.concatenate([np.arange(v * nt, min(n, (v + 1) * nt)) for v in range(0, stages, stride)]) \
+        if n else np.zeros(0, np.int64)
+    sc = queries.astype(np.float64) @ shard[rows].astype(np.float64).T  # [nq, m]
+    m = sc.shape[1]
+    pad = (-m) % group
+    sc = np.concatenate([sc, np.full((sc.shape[0], pad), -np.inf)], axis=1)
+    gmax = sc.reshape(sc.shape[0], -1, group).max(axis=2)
+    top = -np.sort(-gmax, axis=1)[:, :32]
+    if top.shape[1] < 32:
+        top = np.concatenate([top, np.full((top.shape[0], 32 - top.shape[1]), -np.inf)], axis=1)
+    return top.astype(np.float32), (len(range(0, stages, stride)), stages)

@@ -124,6 +124,7 @@ static int g_v4_stride = 0;   // 0: planner's choice
 static int g_v4_rank = -1;    // -1: planner's choice; 0: no sample (v2-style running threshold)
 static int g_v4_joint = 1;    // 1: over several splits, one corpus-wide threshold per query
 static int g_dense = 1;       // 1: fp32 small corpora take the GEMM + select pair (topk_dense.h)
+static int g_v4_presample = 1;  // 1: joint thresholds from one sample-only launch over every split
 
 // log P(Bin(n, f) >= r)
 inline double log_binom_tail(int n, double f, int r) {
@@ -176,6 +177,29 @@ inline void plan_v4_sample(int k, int64_t items_per_split, int& stride, int& ran
     }
 }
 
+// the same, for a sample taken split by split (every stride-th stage of each
+// split: the presampled plan, or shards of a corpus on several GPUs): the
+// sampled fraction is sum_s ceil(stages_s / stride) / stages
+inline void plan_v4_sample_split(int k, int64_t nx, int64_t items_per_split, int& stride, int& rank) {
+    constexpr int NT = v4::Cfg4<__half, 8>::NT;
+    const int64_t nst = (nx + NT - 1) / NT;
+    const int64_t sps = (items_per_split + NT - 1) / NT;  // stages per full split
+    const int64_t nfull = nst / sps, rem = nst - nfull * sps;
+    stride = 0;
+    rank = 0;
+    for (int st = RT_TOPK_V4_MAX_STRIDE; st >= 2; --st) {
+        const int64_t nsa = nfull * ((sps + st - 1) / st) + (rem + st - 1) / st;
+        if (nsa < 4) continue;
+        const double f = static_cast<double>(nsa) / static_cast<double>(nst);
+        for (int r = 1; r <= 2 * v4::kList; ++r) {
+            if (log_binom_tail(k, f, r) <= std::log(1e-6)) {
+                if (r / f <= RT_TOPK_V4_APPEND_CAP) { stride = st; rank = r; return; }
+                break;
+            }
+        }
+    }
+}
+
 // v4 (sampled-threshold scan + finish) for 16-bit, d <= 128, 32 < k <= 128 over
 // a large corpus with enough queries to fill the chip at <= 8 item splits
 inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
@@ -187,7 +211,9 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
     p.chunk = nq < kQueryChunk ? nq : kQueryChunk;
     if (p.chunk < 1) p.chunk = 1;
     p.q_tiles = static_cast<int>((p.chunk + QT - 1) / QT);
-    if (!forced && p.q_tiles < 32) return false;
+    // enough query tiles that <= kMaxSplits item splits fill the chip (the
+    // 8,192-query slice of one of 8 GPUs: 16 tiles x 16 splits)
+    if (!forced && static_cast<int64_t>(p.q_tiles) * v4::kMaxSplits < kCUs) return false;
     int splits = 1;
     while (splits < v4::kMaxSplits && static_cast<int64_t>(p.q_tiles) * splits < kCUs) splits *= 2;
     constexpr int NT = v4::Cfg4<__half, 8>::NT;
@@ -203,13 +229,18 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
     // (the union of the splits' buffers then holds ~rank*stride entries, not
     // splits times that); one split: the per-split form
     p.v4_joint = (p.splits > 1 && g_v4_joint) ? 1 : 0;
-    plan_v4_sample(k, p.v4_joint ? nx : p.items_per_split, p.stride, p.rank);
+    p.v4_presample = (p.v4_joint && g_v4_presample) ? 1 : 0;
+    if (p.v4_presample) plan_v4_sample_split(k, nx, p.items_per_split, p.stride, p.rank);
+    else plan_v4_sample(k, p.v4_joint ? nx : p.items_per_split, p.stride, p.rank);
+    if (p.v4_presample && (p.stride <= 0 || p.rank <= 0)) p.v4_presample = 0;  // no sample fits: round-4 form
     if (g_v4_stride > 0) p.stride = g_v4_stride;
     if (g_v4_rank >= 0) p.rank = g_v4_rank;
     const int64_t q_pad = static_cast<int64_t>(p.q_tiles) * QT;
     p.cand_bytes = static_cast<size_t>(p.splits) * q_pad * v4::kCap * sizeof(Cand);
     p.meta_bytes = static_cast<size_t>(p.splits) * q_pad * 2 * sizeof(int);
     p.fail_bytes = p.v4_joint ? static_cast<size_t>(q_pad) * sizeof(int) : 0;
+    p.lists_bytes = p.v4_presample ? static_cast<size_t>(p.splits) * q_pad * v4::kSampleList * sizeof(float) : 0;
+    p.thr_bytes = p.v4_presample ? static_cast<size_t>(q_pad) * sizeof(float) : 0;
     p.part_bytes = 0;
     return true;
 }
@@ -270,7 +301,7 @@ extern "C" size_t rt_flatip_topk_workspace_bytes(int64_t nq, int64_t nx, int d, 
     if (dtype != RT_F32 && dtype != RT_F16 && dtype != RT_BF16) return 256;
     const topk::Plan p = topk::make_plan(nq, nx, d, dtype, k, topk::shape_for(dtype, d, k));
     return topk::align256(p.cand_bytes) + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes) +
-           topk::align256(p.fail_bytes) + 256;
+           topk::align256(p.fail_bytes) + topk::align256(p.lists_bytes) + topk::align256(p.thr_bytes) + 256;
 }
 
 extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
@@ -290,13 +321,15 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     const size_t cand_al = topk::align256(p.cand_bytes);
     if (!workspace ||
         workspace_bytes < cand_al + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes) +
-                              topk::align256(p.fail_bytes))
+                              topk::align256(p.fail_bytes) + topk::align256(p.lists_bytes) + topk::align256(p.thr_bytes))
         return RT_ERR_WORKSPACE;
     hipStream_t st = as_stream(stream);
     char* part = reinterpret_cast<char*>(workspace) + cand_al;
     int* meta = reinterpret_cast<int*>(part + p.part_bytes);
     uint32_t* kth = reinterpret_cast<uint32_t*>(part + p.part_bytes + topk::align256(p.meta_bytes));
     int* fail = reinterpret_cast<int*>(part + p.part_bytes + topk::align256(p.meta_bytes) + topk::align256(p.kth_bytes));
+    float* v4_lists = reinterpret_cast<float*>(reinterpret_cast<char*>(fail) + topk::align256(p.fail_bytes));
+    float* v4_thr = reinterpret_cast<float*>(reinterpret_cast<char*>(v4_lists) + topk::align256(p.lists_bytes));
     const size_t esz = dtype == RT_F32 ? 4 : 2;
     for (int64_t q0 = 0; q0 < nq; q0 += p.chunk) {
         const int64_t nc = (nq - q0) < p.chunk ? (nq - q0) : p.chunk;
@@ -321,6 +354,8 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
         a.id_offset = id_offset;
         a.meta = meta;
         a.fail = fail;
+        a.v4_lists = v4_lists;
+        a.v4_thr = v4_thr;
         if (p.kth_bytes) {
             a.kth_shared = kth;
             const hipError_t e = hipMemsetAsync(kth, 0, static_cast<size_t>(nc) * sizeof(uint32_t), st);
@@ -350,10 +385,120 @@ extern "C" int rt_flatip_topk(const void* queries, int64_t nq, const void* items
     return RT_OK;
 }
 
+// ---- corpus-sharded search with one corpus-wide threshold per query ----
+// (several GPUs, each holding a row shard: rtrec_amd/dist/sharded.py::
+// sharded_topk_global). Only where rt_flatip_topk plans the v4 kernel pair.
+namespace rt {
+namespace topk {
+struct ShardArgs {
+    Plan p;
+    Args a;
+    size_t need;
+};
+inline int shard_setup(const void* queries, int64_t nq, const void* items, int64_t nx, int d, int dtype, int k,
+                       void* workspace, size_t workspace_bytes, ShardArgs& s) {
+    if (nq <= 0 || nx <= 0 || d <= 0 || k <= 0 || k > v4::kMaxK) return RT_ERR_INVALID;
+    if (dtype != RT_F16 && dtype != RT_BF16) return RT_ERR_UNSUPPORTED;
+    if (d % 8 != 0 || d > 128) return RT_ERR_UNSUPPORTED;
+    if (!queries || !items) return RT_ERR_INVALID;
+    if ((reinterpret_cast<uintptr_t>(queries) | reinterpret_cast<uintptr_t>(items)) & 15) return RT_ERR_INVALID;
+    if (nx >= 0xFFFFFFFFll) return RT_ERR_UNSUPPORTED;
+    s.p = make_plan(nq, nx, d, dtype, k, shape_for(dtype, d, k));
+    if (!s.p.v4 || s.p.chunk < nq) return RT_ERR_UNSUPPORTED;  // one query chunk, the v4 plan
+    const int64_t q_pad = static_cast<int64_t>(s.p.q_tiles) * v4::Geo<v4::kQS>::QT;
+    const size_t lists = static_cast<size_t>(s.p.splits) * q_pad * v4::kSampleList * sizeof(float);
+    s.need = align256(s.p.cand_bytes) + align256(s.p.meta_bytes) + align256(lists) + align256(q_pad * sizeof(float));
+    if (!workspace || workspace_bytes < s.need) return RT_ERR_WORKSPACE;
+    char* w = reinterpret_cast<char*>(workspace);
+    s.a = Args{};
+    s.a.Q = queries;
+    s.a.nq = nq;
+    s.a.X = items;
+    s.a.nx = nx;
+    s.a.d = d;
+    s.a.k = k;
+    s.a.cand = reinterpret_cast<Cand*>(w);
+    s.a.meta = reinterpret_cast<int*>(w + align256(s.p.cand_bytes));
+    s.a.v4_lists = reinterpret_cast<float*>(w + align256(s.p.cand_bytes) + align256(s.p.meta_bytes));
+    return RT_OK;
+}
+inline int v4_scan(int dtype, const Args& a, const Plan& p, int stride, int rank, int mode, hipStream_t st) {
+    return dtype == RT_F16 ? v4_scan_f16(a, p, stride, rank, mode, st) : v4_scan_bf16(a, p, stride, rank, mode, st);
+}
+}  // namespace topk
+}  // namespace rt
+
+extern "C" size_t rt_flatip_topk_shard_workspace_bytes(int64_t nq, int64_t nx, int d, int dtype, int k) {
+    topk::ShardArgs s{};
+    const int rc = topk::shard_setup(reinterpret_cast<const void*>(16), nq, reinterpret_cast<const void*>(16), nx, d,
+                                     dtype, k, reinterpret_cast<void*>(16), ~size_t(0), s);
+    return rc ? 0 : s.need + 256;
+}
+
+extern "C" int rt_flatip_topk_shard_sample(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
+                                           int dtype, int k, int stride, float* top32, int64_t* stage_counts,
+                                           void* workspace, size_t workspace_bytes, void* stream) {
+    topk::ShardArgs s{};
+    int rc = topk::shard_setup(queries, nq, items, nx, d, dtype, k, workspace, workspace_bytes, s);
+    if (rc) return rc;
+    if (stride < 1 || !top32 || !stage_counts) return RT_ERR_INVALID;
+    constexpr int NT = topk::v4::Cfg4<__half, 8>::NT;
+    const int64_t nst = (nx + NT - 1) / NT, sps = (s.p.items_per_split + NT - 1) / NT;
+    const int64_t nfull = nst / sps, rem = nst - nfull * sps;
+    stage_counts[0] = nfull * ((sps + stride - 1) / stride) + (rem + stride - 1) / stride;  // sampled stages
+    stage_counts[1] = nst;
+    hipStream_t st = as_stream(stream);
+    topk::Args b = s.a;
+    b.lists_out = s.a.v4_lists;
+    const int64_t q_pad = static_cast<int64_t>(s.p.q_tiles) * topk::v4::Geo<topk::v4::kQS>::QT;
+    rc = topk::v4_scan(dtype, b, s.p, stride, 1, 3, st);
+    if (rc) return rc;
+    return topk::v4::launch_threshold(s.a.v4_lists, s.p.splits, q_pad * topk::v4::kSampleList, nq, 1, nullptr, top32,
+                                      st);
+}
+
+extern "C" int rt_topk_sample_rank(int k, int64_t sampled_stages, int64_t stages, int* rank) {
+    if (k <= 0 || k > topk::v4::kMaxK || sampled_stages <= 0 || stages < sampled_stages || !rank) return RT_ERR_INVALID;
+    const double f = static_cast<double>(sampled_stages) / static_cast<double>(stages);
+    *rank = 0;  // 0: no failure-safe rank within the lists (the caller scans from -inf)
+    for (int r = 1; r <= topk::v4::kSampleList; ++r)
+        if (topk::log_binom_tail(k, f, r) <= std::log(1e-6)) { *rank = r; break; }
+    return RT_OK;
+}
+
+extern "C" int rt_topk_sample_threshold(const float* lists, int n_lists, int64_t nq, int rank, float* thr,
+                                        void* stream) {
+    if (!lists || !thr || n_lists <= 0 || nq < 0 || rank < 1 || rank > topk::v4::kSampleList) return RT_ERR_INVALID;
+    if (nq == 0) return RT_OK;
+    return topk::v4::launch_threshold(lists, n_lists, nq * topk::v4::kSampleList, nq, rank, thr, nullptr,
+                                      as_stream(stream));
+}
+
+extern "C" int rt_flatip_topk_shard_search(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
+                                           int dtype, int k, const float* thr, int64_t id_offset, float* out_scores,
+                                           int64_t* out_ids, void* workspace, size_t workspace_bytes, void* stream) {
+    topk::ShardArgs s{};
+    int rc = topk::shard_setup(queries, nq, items, nx, d, dtype, k, workspace, workspace_bytes, s);
+    if (rc) return rc;
+    if (!thr || !out_scores || !out_ids || id_offset < 0 || (id_offset + nx) >= 0xFFFFFFFFll) return RT_ERR_INVALID;
+    hipStream_t st = as_stream(stream);
+    topk::Args b = s.a;
+    b.thr_in = thr;
+    b.out_s = out_scores;
+    b.out_i = out_ids;
+    b.id_offset = id_offset;
+    const int64_t q_pad = static_cast<int64_t>(s.p.q_tiles) * topk::v4::Geo<topk::v4::kQS>::QT;
+    rc = topk::v4_scan(dtype, b, s.p, 0, 0, 4, st);
+    if (rc) return rc;
+    return topk::v4::launch_finish(b, s.p.splits, q_pad, 3, nullptr, st);  // no union check: a shard may hold < k
+}
+
 extern "C" int rt_flatip_topk_tuning(int v4_mode, int v4_stride, int v4_rank) {
-    if (v4_mode < 0 || (v4_mode & 3) > 2 || v4_mode > 14 || v4_stride < 0 || v4_rank < -1 ||
+    if (v4_mode < 0 || (v4_mode & 3) > 2 || v4_mode > 30 || v4_stride < 0 || v4_rank < -1 ||
         v4_rank > 2 * topk::v4::kList)
         return RT_ERR_INVALID;
+    topk::g_v4_presample = (v4_mode & 16) ? 0 : 1;
+    v4_mode &= 15;
     topk::g_dense = (v4_mode & 8) ? 0 : 1;
     v4_mode &= 7;
     topk::g_v4_joint = (v4_mode & 4) ? 0 : 1;

@@ -19,6 +19,17 @@ int launch_f16(const Args& a, const Plan& p, hipStream_t st) {
     }
 }
 
+// one v4 scan launch in a given mode (the sharded-search entry points)
+int v4_scan_f16(const Args& a, const Plan& p, int stride, int rank, int mode, hipStream_t st) {
+    switch (s_f16(a.d)) {
+        case 4: return v4::launch_scan<__half, 4, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, stride, rank, a.meta,
+                                                          mode, a.fail, st);
+        case 8: return v4::launch_scan<__half, 8, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, stride, rank, a.meta,
+                                                          mode, a.fail, st);
+        default: return RT_ERR_UNSUPPORTED;
+    }
+}
+
 Shape shape_f16(int d, int k) {
     switch (s_f16(d)) {
         case 4: return shape_S<__half, 4>(k);

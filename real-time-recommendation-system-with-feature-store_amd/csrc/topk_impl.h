@@ -102,6 +102,8 @@ struct Plan {
     int v4_joint;        // v4 over > 1 split: one threshold per query from a corpus-wide sample
     size_t fail_bytes;   // v4 joint: per-query flags (union of the split buffers < k)
     int stride, rank;    // v4 sample: every stride-th stage; threshold = rank-th group maximum
+    int v4_presample;    // v4 joint: one sample-only scan of every split, then the thresholds (launch_presampled)
+    size_t lists_bytes, thr_bytes;  // v4 presampled plan workspaces
     size_t meta_bytes;   // v4 per-(split, query) entry counts
     size_t kth_bytes;    // register-list kernel over > 1 split: the shared per-query k-th keys
     int dense;           // 1: fp32 small corpus, GEMM into a score slab + per-query select (topk_dense.h)
@@ -113,6 +115,10 @@ struct Args {
     Cand* cand; float* out_s; int64_t* out_i; int64_t id_offset;
     int* meta;
     int* fail;             // v4 joint threshold: per-query rescue flags (nullptr: per-split mode)
+    const float* thr_in;   // v4 mode 4: per-query thresholds (a presample's, or a caller's)
+    float* lists_out;      // v4 mode 3: [splits][q_pad][32] sampled group maxima per query
+    float* v4_lists;       // v4 presampled plan: workspace of the mode-3 lists
+    float* v4_thr;         // v4 presampled plan: workspace of the per-query thresholds
     uint32_t* kth_shared;  // register-list kernel, split corpora: per query, the best split k-th score (okey)
 };
 
@@ -467,6 +473,9 @@ template <typename T, int S>
 int launch_S(const Args& a, const Plan& p, hipStream_t st) {
     constexpr bool F32 = sizeof(T) == 4;
     if constexpr (!F32 && S <= 8) {
+        if (p.v4 && p.v4_presample)
+            return v4::launch_presampled<T, S, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank,
+                                                        a.v4_lists, a.v4_thr, a.fail, st);
         if (p.v4)
             return v4::launch_S<T, S, v4::kQS>(a, p.q_tiles, p.splits, p.items_per_split, p.stride, p.rank, a.meta,
                                                p.v4_joint ? a.fail : nullptr, st);
@@ -511,6 +520,8 @@ Shape shape_S(int k) {
 int launch_f32(const Args& a, const Plan& p, hipStream_t st);
 int launch_f16(const Args& a, const Plan& p, hipStream_t st);
 int launch_bf16(const Args& a, const Plan& p, hipStream_t st);
+int v4_scan_f16(const Args& a, const Plan& p, int stride, int rank, int mode, hipStream_t st);
+int v4_scan_bf16(const Args& a, const Plan& p, int stride, int rank, int mode, hipStream_t st);
 Shape shape_f32(int d, int k);
 Shape shape_f16(int d, int k);
 Shape shape_bf16(int d, int k);

@@ -61,7 +61,8 @@ constexpr int kCap = 1024;             // candidate entries per (split, query)
 constexpr int kHalf = kCap / 2;        // per owning lane half
 constexpr int kMaxK = 128;
 constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
-constexpr int kMaxSplits = 8;
+constexpr int kMaxSplits = 16;
+constexpr int kSampleList = 32;       // per query: the 32 largest sampled group maxima (both lane halves)
 constexpr int kFinishCap = 128;        // survivors a finish wave sorts at once (2 per lane)
 constexpr int kFinishRegs = 16;        // candidates per lane the finish holds in registers
 #ifndef RT_TOPK_V4_QS
@@ -118,10 +119,9 @@ __device__ __forceinline__ void list_insert_med3(float (&l)[kList], float x) {
     l[0] = fmaxf(l[0], x);
 }
 
-// the rank-th largest (1-based, rank <= 32) of the union of this lane's list
-// and its partner lane's (lane ^ 32); -inf when fewer finite entries exist
-__device__ __forceinline__ float union_rank(const float (&l)[kList], int rank) {
-    float u[2 * kList];
+// the union of this lane's list and its partner lane's (lane ^ 32), sorted
+// descending into u[0 .. 2 kList)
+__device__ __forceinline__ void union_sorted(const float (&l)[kList], float (&u)[2 * kList]) {
 #pragma unroll
     for (int i = 0; i < kList; ++i) {
         u[i] = l[i];
@@ -138,6 +138,13 @@ __device__ __forceinline__ float union_rank(const float (&l)[kList], int rank) {
             }
         }
     }
+}
+
+// the rank-th largest (1-based, rank <= 32) of the union of this lane's list
+// and its partner lane's (lane ^ 32); -inf when fewer finite entries exist
+__device__ __forceinline__ float union_rank(const float (&l)[kList], int rank) {
+    float u[2 * kList];
+    union_sorted(l, u);
     float v = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 2 * kList; ++i) v = (i == rank - 1) ? u[i] : v;
@@ -290,11 +297,16 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     //   a query derives the same threshold, a lower bound of the query's k-th
     //   over the corpus; no per-split verification (the finish checks the union);
     // mode 2 (rescue): only queries the finish flagged (union < k) run, from -inf.
+    // mode 3 (presample): the sample pass over this block's own split only, its
+    //   32 largest group maxima per query to a.lists_out; no main pass
+    //   (flatip_topk_v4_threshold turns the lists of all splits — or of all
+    //   ranks' shards — into one threshold per query);
+    // mode 4: no sample pass, thr = a.thr_in[query], then the main pass.
     const bool joint = mode == 1;
     // rows [p_begin, p_end) of the current pass (fetch, tail masks, stages)
     int64_t p_begin = joint ? 0 : i_begin, p_end = joint ? a.nx : i_end;
     const int nst_s = joint ? static_cast<int>((a.nx + C::NT - 1) / C::NT) : nst;
-    const int nsa = (mode != 2 && rank > 0 && stride > 0) ? (nst_s + stride - 1) / stride : 0;  // sample stages
+    const int nsa = (mode != 2 && mode != 4 && rank > 0 && stride > 0) ? (nst_s + stride - 1) / stride : 0;  // sample stages
     if (tid == 0) *flag = 0u;
     if (mode == 2) {  // rescue: exit before any load unless a query of this block was flagged
         __syncthreads();  // *flag zeroed above
@@ -356,6 +368,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     if (mode == 2) {  // rescue: the flagged queries from -inf (a running threshold), the rest skip
 #pragma unroll
         for (int j = 0; j < QS; ++j) thr[j] = (qok[j] && fail[qw + j * 32 + col] != 0) ? -FLT_MAX : INFINITY;
+    }
+    if (mode == 4) {  // external per-query thresholds (a presample over every split / every shard)
+#pragma unroll
+        for (int j = 0; j < QS; ++j) thr[j] = qok[j] ? fmaxf(a.thr_in[qw + j * 32 + col], -FLT_MAX) : INFINITY;
     }
     constexpr int kHead = C::NSUB * 16;  // appends per half between two compaction checks, at most
     constexpr uint32_t kLimBytes = static_cast<uint32_t>((kHalf - kHead) * sizeof(Cand));
@@ -607,11 +623,37 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             cur = cur == C::RING - 1 ? 0 : cur + 1;
         }
         RT_PT(pc_samp = clock64() - pc_start;)
+        if (mode == 3) {  // presample: the split's 32 largest group maxima per query, sorted
+#pragma unroll
+            for (int j = 0; j < QS; ++j) {
+                float u[2 * kList];
+                union_sorted(L[j], u);
+                if (half == 0 && qok[j]) {
+                    float4* o = reinterpret_cast<float4*>(
+                        a.lists_out + ((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * kSampleList);
+#pragma unroll
+                    for (int i = 0; i < kSampleList / 4; ++i)
+                        o[i] = make_float4(u[4 * i], u[4 * i + 1], u[4 * i + 2], u[4 * i + 3]);
+                }
+            }
+            return;  // block-uniform: mode 3 runs no main pass
+        }
 #pragma unroll
         for (int j = 0; j < QS; ++j) {
             const float e = union_rank(L[j], rank);
             if (qok[j]) thr[j] = e > -FLT_MAX ? e : -FLT_MAX;
         }
+    }
+    if (mode == 3) {  // an empty split (no sample stages): no candidates to report
+#pragma unroll
+        for (int j = 0; j < QS; ++j)
+            if (half == 0 && qok[j]) {
+                float4* o = reinterpret_cast<float4*>(
+                    a.lists_out + ((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * kSampleList);
+#pragma unroll
+                for (int i = 0; i < kSampleList / 4; ++i) o[i] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+            }
+        return;
     }
     p_begin = i_begin;  // the main pass covers this block's split
     p_end = i_end;
@@ -962,6 +1004,99 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
     if (m > kFinishCap) m = kFinishCap;  // cannot happen: the prefix bounds it
     wave_lds_sync();
     finish_sort<2>(keep, m, k, os, oi, id_offset);
+}
+
+// per query: the rank-th largest (1-based, rank <= 32) of the union of
+// n_lists sorted 32-entry lists (list l of query q at lists[l * list_stride +
+// q * 32]) -> thr[q] (-FLT_MAX when the union has fewer finite entries: a
+// running threshold), and/or the union's 32 largest, sorted, -> top[q * 32].
+// One wave per query, n_lists * 32 <= 64 * E entries sorted in registers.
+template <int E>
+__global__ __launch_bounds__(256) void flatip_topk_v4_threshold(const float* __restrict__ lists, int n_lists,
+                                                                int64_t list_stride, int64_t nq, int rank,
+                                                                float* __restrict__ thr, float* __restrict__ top) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    float v[E];
+    uint32_t id[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+        const int e = lane * E + j, l = e / kSampleList;
+        v[j] = l < n_lists ? lists[static_cast<int64_t>(l) * list_stride + q * kSampleList + (e % kSampleList)]
+                           : -INFINITY;
+        id[j] = static_cast<uint32_t>(e);
+    }
+    wave_sort_regs<E>(v, id);
+    if (thr) {
+        const int r = rank - 1;
+        const float x = __shfl(v[r % E], r / E, 64);
+        if (lane == 0) thr[q] = x > -FLT_MAX ? x : -FLT_MAX;
+    }
+    if (top) {
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+            if (lane * E + j < kSampleList) top[q * kSampleList + lane * E + j] = v[j];
+    }
+}
+
+inline int launch_threshold(const float* lists, int n_lists, int64_t list_stride, int64_t nq, int rank, float* thr,
+                            float* top, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>((nq + 3) / 4));
+    if (n_lists * kSampleList <= 128)
+        hipLaunchKernelGGL(flatip_topk_v4_threshold<2>, grid, dim3(256), 0, st, lists, n_lists, list_stride, nq, rank,
+                           thr, top);
+    else if (n_lists * kSampleList <= 256)
+        hipLaunchKernelGGL(flatip_topk_v4_threshold<4>, grid, dim3(256), 0, st, lists, n_lists, list_stride, nq, rank,
+                           thr, top);
+    else if (n_lists * kSampleList <= 512)
+        hipLaunchKernelGGL(flatip_topk_v4_threshold<8>, grid, dim3(256), 0, st, lists, n_lists, list_stride, nq, rank,
+                           thr, top);
+    else
+        return RT_ERR_UNSUPPORTED;
+    return check_launch("flatip_topk_v4_threshold");
+}
+
+template <typename T, int S, int QS>
+int launch_scan(const Args& a, int q_tiles, int splits, int64_t items_per_split, int stride, int rank, int* meta,
+                int mode, int* fail, hipStream_t st) {
+    dim3 grid(static_cast<unsigned>(q_tiles * splits));
+    if (a.excl)
+        hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, true>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                           items_per_split, stride, rank, meta, mode, fail);
+    else
+        hipLaunchKernelGGL((flatip_topk_v4_scan<T, S, QS, false>), grid, dim3(64 * kWavesB), 0, st, a, splits,
+                           items_per_split, stride, rank, meta, mode, fail);
+    return check_launch("flatip_topk_v4_scan");
+}
+
+inline int launch_finish(const Args& a, int splits, int64_t q_pad, int mode, int* fail, hipStream_t st) {
+    hipLaunchKernelGGL(flatip_topk_v4_finish<4>, dim3(static_cast<unsigned>((a.nq + 3) / 4)), dim3(256), 0, st,
+                       a.cand, a.meta, splits, q_pad, a.nq, a.k, a.out_s, a.out_i, a.id_offset, mode, fail);
+    return check_launch("flatip_topk_v4_finish");
+}
+
+// presampled joint threshold (several splits): a sample-only scan of every
+// split (mode 3), the per-query threshold from the union of the split lists,
+// the main scan against it (mode 4), the finish with the union check (mode
+// 1), then the rescue pair (mode 2) — every block samples its own split only
+// (the mode-1 scan has every block sample the whole corpus)
+template <typename T, int S, int QS>
+int launch_presampled(const Args& a, int q_tiles, int splits, int64_t items_per_split, int stride, int rank,
+                      float* lists, float* thr, int* fail, hipStream_t st) {
+    const int64_t q_pad = static_cast<int64_t>(q_tiles) * Geo<QS>::QT;
+    Args b = a;
+    b.lists_out = lists;
+    int rc = launch_scan<T, S, QS>(b, q_tiles, splits, items_per_split, stride, rank, a.meta, 3, nullptr, st);
+    if (rc) return rc;
+    if ((rc = launch_threshold(lists, splits, q_pad * kSampleList, a.nq, rank, thr, nullptr, st))) return rc;
+    b.lists_out = nullptr;
+    b.thr_in = thr;
+    if ((rc = launch_scan<T, S, QS>(b, q_tiles, splits, items_per_split, stride, rank, a.meta, 4, nullptr, st)))
+        return rc;
+    if ((rc = launch_finish(a, splits, q_pad, 1, fail, st))) return rc;
+    if ((rc = launch_scan<T, S, QS>(a, q_tiles, splits, items_per_split, stride, rank, a.meta, 2, fail, st))) return rc;
+    return launch_finish(a, splits, q_pad, 2, fail, st);
 }
 
 template <typename T, int S, int QS>

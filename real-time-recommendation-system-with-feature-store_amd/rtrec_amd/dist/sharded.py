@@ -125,6 +125,122 @@ def sharded_topk_owner(queries: torch.Tensor, k: int, local_topk: TopkFn, merge:
     return merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
 
 
+class ShardOps:
+    """Per-rank compute of :func:`sharded_topk_global` over one row shard
+    (``shard`` [rows, d], global row ``begin``), bound to the HIP kernels;
+    tests substitute CPU versions of the same five callables."""
+
+    def __init__(self, shard: torch.Tensor, begin: int):
+        self.shard, self.begin = shard, int(begin)
+
+    def sample(self, q, k, stride):
+        return kernels.flatip_topk_shard_sample(q, self.shard, k, stride)
+
+    def rank(self, k, sampled, stages):
+        return kernels.topk_sample_rank(k, sampled, stages)
+
+    def threshold(self, lists, rank):
+        return kernels.topk_sample_threshold(lists, rank)
+
+    def search(self, q, k, thr):
+        return kernels.flatip_topk_shard_search(q, self.shard, k, thr, id_offset=self.begin)
+
+    def topk(self, q, k):
+        return kernels.flatip_topk(q, self.shard, k, id_offset=self.begin)
+
+
+LAST_TOPK: dict = {}  # the latest sharded_topk_global call: path, rank, rescued queries
+
+
+def sharded_topk_global(queries: torch.Tensor, k: int, n_total: int, ops, merge: MergeFn, group=None,
+                        owner: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Exact top-k over a row-sharded corpus with ONE corpus-wide threshold
+    per query (rt_flatip_topk_shard_* of include/rtrec_hip.h).
+
+    1. every rank samples its shard (every stride-th 128-row stage: per query
+       the 32 largest group maxima, ``ops.sample``); one all-gather of the
+       [nq, 32] lists and one 24-byte all-reduce of the stage counts;
+    2. the failure-safe rank for the corpus-wide sampled fraction
+       (``ops.rank``) and per query the rank-th largest of the union of all
+       ranks' lists (``ops.threshold``) — w.h.p. at most the query's k-th score
+       over the WHOLE corpus;
+    3. each rank keeps only its rows at or above it (``ops.search``): a query's
+       candidates per shard shrink as the shards multiply, where a
+       shard-local threshold keeps ~k per shard (:func:`sharded_topk_owner`);
+    4. the per-rank lists are merged as in :func:`sharded_topk_owner`
+       (``owner``: all-to-all, each rank its slice of the queries) or
+       :func:`sharded_topk` (all-gather, every rank all queries);
+    5. a query whose merged list holds fewer than min(k, n_total) entries had a
+       threshold above its k-th: those queries (host-read flags, P < 1e-6
+       each) are searched again from -inf through :func:`sharded_topk`.
+    Identical to one index over the whole corpus (scores depend only on the
+    (query, row) pair). Shapes without the v4 plan on some rank take the
+    plain path (``ops.topk``) on every rank."""
+    world, rank = _world(group)
+    nq = queries.shape[0]
+    plain = sharded_topk_owner if owner else sharded_topk
+    if world == 1:
+        return ops.topk(queries, k)
+    if owner and nq % world:
+        raise ValueError(f"{nq} queries do not split over {world} ranks")
+    stride = kernels.shard_sample_stride(n_total)
+    smp = ops.sample(queries, k, stride)
+    dev = queries.device
+    cnt = torch.tensor([1 if smp is not None else 0, smp[1][0] if smp else 0, smp[1][1] if smp else 0],
+                       dtype=torch.int64, device=dev)
+    dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+    supported, sampled, stages = (int(v) for v in cnt.tolist())
+    if supported != world:
+        LAST_TOPK.clear()
+        LAST_TOPK.update({"path": "plain (no v4 plan on some shard)"})
+        return plain(queries, k, ops.topk, merge, group)
+    top = smp[0].contiguous()
+    lists = torch.empty((world * nq, top.shape[1]), dtype=top.dtype, device=dev)
+    dist.all_gather_into_tensor(lists, top, group=group)
+    r = ops.rank(k, sampled, stages)
+    if r > 0:
+        thr = ops.threshold(lists.view(world, nq, top.shape[1]), r)
+    else:
+        thr = torch.full((nq,), -3.4028234663852886e38, dtype=torch.float32, device=dev)
+    s, i = ops.search(queries, k, thr)
+    if owner:
+        s, i = s.contiguous(), i.contiguous()
+        out_s, out_i = torch.empty_like(s), torch.empty_like(i)
+        dist.all_to_all_single(out_s, s, group=group)
+        dist.all_to_all_single(out_i, i, group=group)
+        per = nq // world
+        ms, mi = merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
+    else:
+        all_s, all_i = all_gather_candidates(s, i, group)
+        ms, mi = merge(all_s, all_i, k)
+    need = min(int(k), int(n_total))
+    bad = ((mi >= 0).sum(dim=1) < need).to(torch.uint8)
+    if owner:
+        allbad = torch.empty(world * bad.numel(), dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(allbad, bad.contiguous(), group=group)
+    else:
+        allbad = bad
+    idx = torch.nonzero(allbad).flatten()
+    n_bad = int(idx.numel())
+    if n_bad:
+        fs, fi = sharded_topk(queries.index_select(0, idx), k, ops.topk, merge, group)
+        if owner:
+            per = nq // world
+            mine = (idx >= rank * per) & (idx < (rank + 1) * per)
+            rows = idx[mine] - rank * per
+            ms, mi = ms.clone(), mi.clone()
+            ms[rows] = fs[mine]
+            mi[rows] = fi[mine]
+        else:
+            ms, mi = ms.clone(), mi.clone()
+            ms[idx] = fs
+            mi[idx] = fi
+    LAST_TOPK.clear()
+    LAST_TOPK.update({"path": "global threshold", "stride": stride, "rank": r, "sampled_stages": sampled,
+                      "stages": stages, "rescued_queries": n_bad})
+    return ms, mi
+
+
 def _exchange_rows(local: torch.Tensor, group) -> torch.Tensor:
     """Every rank holds [P, D] rows that are zero except at the positions it owns
     (exactly one owner per valid position): the max over ranks of the raw BYTES

@@ -172,6 +172,77 @@ def _flatip_topk_wide(queries, items, k, exclude_bits, id_offset, out):
     return scores, ids
 
 
+# ---- corpus-sharded search with one corpus-wide threshold per query -------
+def shard_sample_stride(n_total: int, nt: int = 128, max_stride: int = 64) -> int:
+    """Sampling stride (in 128-row stages) for a corpus of ``n_total`` rows
+    spread over shards: the planner's 64 when the corpus holds >= 32 x 64
+    stages, else fewer, so that >= 32 stages are sampled in all."""
+    stages = max(1, -(-int(n_total) // nt))
+    return int(max(1, min(max_stride, stages // 32)))
+
+
+def flatip_topk_shard_sample(queries: torch.Tensor, items: torch.Tensor, k: int, stride: int):
+    """This shard's sample (rt_flatip_topk_shard_sample): per query the 32
+    largest sampled group maxima [nq, 32] f32 (descending) and the (sampled,
+    total) 128-row stage counts of the shard. None when the shape has no v4
+    plan (f16/bf16, d <= 128, k <= 128, >= 65,536 rows or forced)."""
+    native.require_device(queries, items, what="flatip_topk_shard_sample")
+    queries, items = queries.contiguous(), items.contiguous()
+    nq, d = queries.shape
+    dt = native.dtype_code(queries.dtype)
+    lib = native.lib()
+    nbytes = lib.rt_flatip_topk_shard_workspace_bytes(nq, items.shape[0], d, dt, k)
+    if nbytes == 0:
+        return None
+    ws = workspace(queries.device, nbytes, "topk_shard")
+    top = torch.empty((nq, 32), dtype=torch.float32, device=queries.device)
+    counts = (ctypes.c_int64 * 2)()
+    call("rt_flatip_topk_shard_sample", ptr(queries), nq, ptr(items), items.shape[0], d, dt, k, int(stride), ptr(top),
+         ctypes.cast(counts, ctypes.c_void_p), ptr(ws), ws.numel(), stream_of(queries))
+    return top, (int(counts[0]), int(counts[1]))
+
+
+def topk_sample_rank(k: int, sampled: int, stages: int) -> int:
+    """Failure-safe rank of a corpus-wide sample (rt_topk_sample_rank): P(the
+    rank-th largest sampled group maximum exceeds the k-th score) < 1e-6;
+    0 when no rank <= 32 is safe (search from -inf)."""
+    r = ctypes.c_int(0)
+    call("rt_topk_sample_rank", int(k), int(sampled), int(stages), ctypes.byref(r))
+    return int(r.value)
+
+
+def topk_sample_threshold(lists: torch.Tensor, rank: int) -> torch.Tensor:
+    """thr [nq] = the rank-th largest of the union of lists [n_lists, nq, 32]
+    (rt_topk_sample_threshold); -FLT_MAX when fewer finite entries."""
+    native.require_device(lists, what="topk_sample_threshold")
+    lists = lists.contiguous()
+    n_lists, nq = lists.shape[0], lists.shape[1]
+    thr = torch.empty(nq, dtype=torch.float32, device=lists.device)
+    call("rt_topk_sample_threshold", ptr(lists), n_lists, nq, int(rank), ptr(thr), stream_of(lists))
+    return thr
+
+
+def flatip_topk_shard_search(queries: torch.Tensor, items: torch.Tensor, k: int, thr: torch.Tensor,
+                             id_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """This shard's rows scoring >= thr[q], the best k per query in (score desc,
+    id asc) order, (-FLT_MAX, -1) padded (rt_flatip_topk_shard_search)."""
+    native.require_device(queries, items, thr, what="flatip_topk_shard_search")
+    queries, items, thr = queries.contiguous(), items.contiguous(), thr.contiguous().float()
+    nq, d = queries.shape
+    dt = native.dtype_code(queries.dtype)
+    nbytes = native.lib().rt_flatip_topk_shard_workspace_bytes(nq, items.shape[0], d, dt, k)
+    if nbytes == 0:
+        raise native.RTError("rt_flatip_topk_shard_search", -2, "no v4 plan for this shape")
+    ws = workspace(queries.device, nbytes, "topk_shard")
+    scores = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
+    ids = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+    with TIMER.region("flatip_topk", flops=2.0 * nq * items.shape[0] * d,
+                      bytes_=float((nq + items.shape[0]) * d * queries.element_size() + nq * k * 12)):
+        call("rt_flatip_topk_shard_search", ptr(queries), nq, ptr(items), items.shape[0], d, dt, k, ptr(thr),
+             int(id_offset), ptr(scores), ptr(ids), ptr(ws), ws.numel(), stream_of(queries))
+    return scores, ids
+
+
 def topk_tuning(v4_mode: int = 0, v4_stride: int = 0, v4_rank: int = -1) -> None:
     """Planner override of flatip_topk (rt_flatip_topk_tuning; process-wide,
     results unchanged): v4_mode 0 automatic / 1 never / 2 wherever legal the

@@ -84,6 +84,13 @@ SIGNATURES = {
                                c_size, vp]),
     "rt_topk_merge": (c_int, [vp, vp, c_i64, c_int, c_int, c_int, vp, vp, vp]),
     "rt_flatip_topk_tuning": (c_int, [c_int, c_int, c_int]),
+    "rt_flatip_topk_shard_workspace_bytes": (c_size, [c_i64, c_i64, c_int, c_int, c_int]),
+    "rt_flatip_topk_shard_sample": (c_int, [vp, c_i64, vp, c_i64, c_int, c_int, c_int, c_int, vp, vp, vp, c_size,
+                                            vp]),
+    "rt_topk_sample_rank": (c_int, [c_int, c_i64, c_i64, vp]),
+    "rt_topk_sample_threshold": (c_int, [vp, c_int, c_i64, c_int, vp, vp]),
+    "rt_flatip_topk_shard_search": (c_int, [vp, c_i64, vp, c_i64, c_int, c_int, c_int, vp, c_i64, vp, vp, vp,
+                                            c_size, vp]),
     "rt_sample_negatives": (c_int, [vp, vp, c_i64, vp, c_i64, c_i64, c_int, c_u64, vp, vp, vp]),
     "rt_feeder_batch": (c_int, [vp, vp, vp, vp, c_i64, vp, vp, vp]),
     "rt_feeder_commit": (c_int, [vp, vp, c_i64, vp, vp]),

@@ -326,3 +326,77 @@ def _c5_worker(rank, world, n, d, b, seed):
 
 def test_sharded_inbatch_step_gloo():
     _run(2, _c5_worker, 401, 16, 24, 5)
+
+
+def _global_thr_worker(rank, world, n, d, nq, k, seed, owner, force_rescue):
+    from rtrec_amd.dist.sharded import LAST_TOPK, sharded_topk_global
+    from rtrec_amd import kernels as K
+    rng = np.random.default_rng(seed)
+    corpus = _dyadic(rng, n, d)
+    corpus[n - 1] = corpus[0]  # a tie across the shard boundary
+    queries = _dyadic(rng, nq, d)
+    b, c = shard_range(n, world, rank)
+    shard = corpus[b:b + c]
+
+    class Ops:  # CPU restatements of the five per-rank calls (tests may use the oracle)
+        def sample(self, q, kk, stride):
+            top, cnt = orc.shard_sample(q.numpy(), shard, stride)
+            return torch.from_numpy(top), cnt
+
+        def rank(self, kk, sampled, stages):
+            return 1 if force_rescue else orc.sample_rank(kk, sampled, stages)
+
+        def threshold(self, lists, r):
+            u = -np.sort(-lists.numpy().transpose(1, 0, 2).reshape(lists.shape[1], -1), axis=1)
+            t = u[:, r - 1]
+            return torch.from_numpy(np.where(np.isfinite(t), t, -np.finfo(np.float32).max).astype(np.float32))
+
+        def search(self, q, kk, thr):
+            sc = (q.numpy().astype(np.float64) @ shard.astype(np.float64).T).astype(np.float32)
+            out_s = np.full((q.shape[0], kk), -np.finfo(np.float32).max, np.float32)
+            out_i = np.full((q.shape[0], kk), -1, np.int64)
+            for r in range(q.shape[0]):
+                keep = np.nonzero(sc[r] >= thr[r].item())[0]
+                order = keep[np.lexsort((keep, -sc[r][keep]))][:kk]
+                out_s[r, :order.size] = sc[r][order]
+                out_i[r, :order.size] = order + b
+            return torch.from_numpy(out_s), torch.from_numpy(out_i)
+
+        def topk(self, q, kk):
+            s, i = orc.flat_ip_search(q.numpy(), shard, kk, id_offset=b)
+            return torch.from_numpy(s), torch.from_numpy(i)
+
+    def merge(s, i, kk):
+        ms, mi = orc.topk_merge(s.numpy(), i.numpy(), kk)
+        return torch.from_numpy(ms), torch.from_numpy(mi)
+
+    got_s, got_i = sharded_topk_global(torch.from_numpy(queries), k, n, Ops(), merge, owner=owner)
+    if owner:
+        qb, qc = shard_range(nq, world, rank)
+        ref_s, ref_i = orc.flat_ip_search(queries[qb:qb + qc], corpus, k)
+    else:
+        ref_s, ref_i = orc.flat_ip_search(queries, corpus, k)
+    np.testing.assert_array_equal(got_i.numpy(), ref_i)
+    np.testing.assert_array_equal(got_s.numpy(), ref_s)
+    assert LAST_TOPK["path"] == "global threshold"
+    assert LAST_TOPK["stride"] == K.shard_sample_stride(n)
+    if force_rescue:
+        assert LAST_TOPK["rescued_queries"] > 0
+
+
+@pytest.mark.parametrize("world,n,k,owner,force", [(2, 16384, 10, True, False), (3, 16384, 100, False, False),
+                                                   (4, 9000, 50, True, False), (2, 16384, 100, True, True)])
+def test_sharded_topk_global_threshold_gloo(world, n, k, owner, force):
+    """C4 at N GPUs with ONE corpus-wide threshold per query (ranks' shard
+    samples all-gathered, the failure-safe rank of the corpus-wide sampled
+    fraction): exact against one index over the whole corpus, owner and
+    all-gather layouts; forcing an unsafe rank (threshold above the k-th)
+    exercises the rescue of the short queries from -inf."""
+    _run(world, _global_thr_worker, n, 32, 24, k, 13, owner, force)
+
+
+def test_sample_rank_matches_library():
+    """oracle.sample_rank restates rt_topk_sample_rank (host code of the library)."""
+    from rtrec_amd import kernels as K
+    for k, s, t in [(100, 122, 7813), (10, 16, 977), (100, 2, 977), (50, 40, 40), (128, 31, 1000)]:
+        assert K.topk_sample_rank(k, s, t) == orc.sample_rank(k, s, t), (k, s, t)

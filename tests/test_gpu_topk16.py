@@ -193,3 +193,73 @@ def test_topk16_v4_full_query_chunk_vs_v2(K, dtype):
         K.topk_tuning(0, 0, -1)
     assert torch.equal(gi, ri)
     assert torch.equal(gs, rs)
+
+
+def test_topk16_v4_sixteen_splits_presampled(K, V4):
+    """8,192 queries (16 query tiles) over a 200K-row corpus: the planner
+    spreads the items over 16 splits (256 blocks), the joint threshold comes
+    from the presample launch (every split sampled once, then one threshold
+    per query), the finish merges 32 split segments per query. Whole-result
+    properties plus a 512-query sample bit-exact against the oracle."""
+    V4(mode=2)
+    g = torch.Generator(device="cuda").manual_seed(21)
+    nq, nx, d, k = 8192, 200_000, 64, 100
+    q = (torch.randint(-64, 65, (nq, d), device="cuda", generator=g) / 64).half()
+    x = (torch.randint(-64, 65, (nx, d), device="cuda", generator=g) / 64).half()
+    gs, gi = K.flatip_topk(q, x, k)
+    torch.cuda.synchronize()
+    assert (gi >= 0).all() and (gi < nx).all()
+    assert (gs[:, :-1] >= gs[:, 1:]).all()
+    sel = torch.randperm(nq, generator=torch.Generator().manual_seed(1))[:512].numpy()
+    rs, ri = orc.flat_ip_search(np.ascontiguousarray(q.float().cpu().numpy()[sel]), x.float().cpu().numpy(), k,
+                                nthreads=16)
+    assert np.array_equal(gi.cpu().numpy()[sel], ri)
+    assert np.array_equal(gs.cpu().numpy()[sel], rs)
+
+
+@pytest.mark.parametrize("n_shards,nx,k", [(8, 400_000, 100), (4, 300_000, 64), (2, 140_000, 128)])
+def test_shard_global_threshold_emulated(K, V4, n_shards, nx, k):
+    """rt_flatip_topk_shard_* as N ranks would run them, all on one GPU: each
+    shard sampled (shard_sample), the lists combined into one threshold per
+    query (topk_sample_threshold with the failure-safe rank of the
+    corpus-wide sampled fraction), each shard searched against it
+    (shard_search), the lists merged (topk_merge): bit-exact against the
+    oracle on dyadic data (scores exact in fp32), every query's merged list
+    full (no rescue needed at this rank), and each shard's candidates far
+    fewer than its own k."""
+    from rtrec_amd.dist.sharded import shard_range
+    V4(mode=2)  # shards below the planner's 65,536-row bound keep the v4 plan
+    g = torch.Generator(device="cuda").manual_seed(5 + n_shards)
+    nq, d = 65536, 128
+    q = (torch.randint(-64, 65, (nq, d), device="cuda", generator=g) / 64).half()
+    x = (torch.randint(-64, 65, (nx, d), device="cuda", generator=g) / 64).half()
+    stride = K.shard_sample_stride(nx)
+    tops, sampled, stages, spans = [], 0, 0, []
+    for r in range(n_shards):
+        b, c = shard_range(nx, n_shards, r)
+        spans.append((b, c))
+        top, (sa, st) = K.flatip_topk_shard_sample(q, x[b:b + c], k, stride)
+        assert top.shape == (nq, 32) and (top[:, :-1] >= top[:, 1:]).all()
+        tops.append(top)
+        sampled += sa
+        stages += st
+    rank = K.topk_sample_rank(k, sampled, stages)
+    assert rank > 0
+    thr = K.topk_sample_threshold(torch.stack(tops), rank)
+    ss, ii = [], []
+    for b, c in spans:
+        s, i = K.flatip_topk_shard_search(q, x[b:b + c], k, thr, id_offset=b)
+        ss.append(s)
+        ii.append(i)
+        valid = i >= 0
+        assert (s[valid] >= thr.unsqueeze(1).expand_as(s)[valid]).all()
+    ms, mi = K.topk_merge(torch.stack(ss), torch.stack(ii), k)
+    torch.cuda.synchronize()
+    assert (mi >= 0).all(), "a threshold above a query's k-th score (needs the rescue)"
+    per_shard = torch.stack([(i >= 0).sum(dim=1).float().mean() for i in ii]).mean().item()
+    assert per_shard < k, per_shard  # candidates per shard shrink below k
+    sel = torch.randperm(nq, generator=torch.Generator().manual_seed(2))[:256].numpy()
+    rs, ri = orc.flat_ip_search(np.ascontiguousarray(q.float().cpu().numpy()[sel]), x.float().cpu().numpy(), k,
+                                nthreads=16)
+    assert np.array_equal(mi.cpu().numpy()[sel], ri)
+    assert np.array_equal(ms.cpu().numpy()[sel], rs)
