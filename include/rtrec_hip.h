@@ -107,8 +107,8 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
  *     for the sampled fraction sum(sampled) / sum(stages) over all shards
  *     (0 = none fits: search from -inf).
  *   rt_topk_sample_threshold: thr[q] = the rank-th largest of the union of
- *     n_lists such lists (layout [n_lists][nq][32], e.g. all-gathered over
- *     ranks); -FLT_MAX when the union has fewer finite entries.
+ *     n_lists (<= 64) such lists (layout [n_lists][nq][32], e.g. all-gathered
+ *     over ranks); -FLT_MAX when the union has fewer finite entries.
  *   rt_flatip_topk_shard_search: this shard's rows with score >= thr[q], the
  *     best k of them per query in (score desc, id asc) order, padded with
  *     (-FLT_MAX, -1) when fewer pass. The caller merges the shards' lists;

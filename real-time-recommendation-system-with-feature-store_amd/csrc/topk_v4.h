@@ -1007,53 +1007,62 @@ __global__ __launch_bounds__(256) void flatip_topk_v4_finish(const Cand* __restr
 }
 
 // per query: the rank-th largest (1-based, rank <= 32) of the union of
-// n_lists sorted 32-entry lists (list l of query q at lists[l * list_stride +
-// q * 32]) -> thr[q] (-FLT_MAX when the union has fewer finite entries: a
-// running threshold), and/or the union's 32 largest, sorted, -> top[q * 32].
-// One wave per query, n_lists * 32 <= 64 * E entries sorted in registers.
-template <int E>
+// n_lists (<= 64) sorted 32-entry lists (list l of query q at lists[l *
+// list_stride + q * 32]) -> thr[q] (-FLT_MAX when the union has fewer finite
+// entries: a running threshold), and/or the union's 32 largest, sorted, ->
+// top[q * 32]. A W-lane group per query (W = 16 for <= 16 lists, else 64),
+// 256 / W queries per block: the group's lists are staged in LDS, lane l
+// holds the head of list l, and each round takes the group maximum (log2 W
+// shuffles) and advances the winning head — rank rounds of a k-way merge
+// instead of sorting all n_lists * 32 values.
+template <int W>
 __global__ __launch_bounds__(256) void flatip_topk_v4_threshold(const float* __restrict__ lists, int n_lists,
                                                                 int64_t list_stride, int64_t nq, int rank,
                                                                 float* __restrict__ thr, float* __restrict__ top) {
-    const int lane = threadIdx.x & 63;
-    const int64_t q = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-    if (q >= nq) return;
-    float v[E];
-    uint32_t id[E];
+    constexpr int QB = 256 / W;                            // queries per block
+    __shared__ float stage[QB][W][kSampleList + 1];        // [query in block][list][entry] (+1: bank spread)
+    const int t = threadIdx.x, g = t / W, l = t % W;
+    const int64_t q0 = static_cast<int64_t>(blockIdx.x) * QB;
+    // coalesced staging: for each list, the block's QB queries x 32 entries are contiguous
+    // (only the n_lists real lists; lanes past them start exhausted)
+    for (int e = t; e < n_lists * QB * kSampleList; e += 256) {
+        const int li = e / (QB * kSampleList), r = e - li * (QB * kSampleList), qi = r / kSampleList,
+                  j = r - qi * kSampleList;
+        stage[qi][li][j] =
+            q0 + qi < nq ? lists[static_cast<int64_t>(li) * list_stride + (q0 + qi) * kSampleList + j] : -INFINITY;
+    }
+    __syncthreads();
+    const int64_t q = q0 + g;
+    int h = l < n_lists ? 0 : kSampleList;
+    float v = l < n_lists ? stage[g][l][0] : -INFINITY;
+    const int rounds = top ? kSampleList : rank;
+    float kth = -INFINITY;
+    const int base = (t & 63) & ~(W - 1);  // the group's first lane within the wave
+    constexpr uint64_t kGroupMask = W == 64 ? ~0ull : (1ull << W) - 1;
+    for (int it = 0; it < rounds; ++it) {
+        float m = v;
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-        const int e = lane * E + j, l = e / kSampleList;
-        v[j] = l < n_lists ? lists[static_cast<int64_t>(l) * list_stride + q * kSampleList + (e % kSampleList)]
-                           : -INFINITY;
-        id[j] = static_cast<uint32_t>(e);
+        for (int o = W / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, W));
+        const uint64_t eq = (__ballot(v == m) >> base) & kGroupMask;
+        if (eq && l == __builtin_ctzll(eq)) {  // eq == 0 only for an all-NaN group: no head moves
+            ++h;
+            v = h < kSampleList ? stage[g][l][h] : -INFINITY;
+        }
+        if (it == rank - 1) kth = m;
+        if (top && l == 0 && q < nq) top[q * kSampleList + it] = m;
     }
-    wave_sort_regs<E>(v, id);
-    if (thr) {
-        const int r = rank - 1;
-        const float x = __shfl(v[r % E], r / E, 64);
-        if (lane == 0) thr[q] = x > -FLT_MAX ? x : -FLT_MAX;
-    }
-    if (top) {
-#pragma unroll
-        for (int j = 0; j < E; ++j)
-            if (lane * E + j < kSampleList) top[q * kSampleList + lane * E + j] = v[j];
-    }
+    if (thr && l == 0 && q < nq) thr[q] = kth > -FLT_MAX ? kth : -FLT_MAX;
 }
 
 inline int launch_threshold(const float* lists, int n_lists, int64_t list_stride, int64_t nq, int rank, float* thr,
                             float* top, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>((nq + 3) / 4));
-    if (n_lists * kSampleList <= 128)
-        hipLaunchKernelGGL(flatip_topk_v4_threshold<2>, grid, dim3(256), 0, st, lists, n_lists, list_stride, nq, rank,
-                           thr, top);
-    else if (n_lists * kSampleList <= 256)
-        hipLaunchKernelGGL(flatip_topk_v4_threshold<4>, grid, dim3(256), 0, st, lists, n_lists, list_stride, nq, rank,
-                           thr, top);
-    else if (n_lists * kSampleList <= 512)
-        hipLaunchKernelGGL(flatip_topk_v4_threshold<8>, grid, dim3(256), 0, st, lists, n_lists, list_stride, nq, rank,
-                           thr, top);
+    if (n_lists < 1 || n_lists > 64) return RT_ERR_UNSUPPORTED;
+    if (n_lists <= 16)
+        hipLaunchKernelGGL(flatip_topk_v4_threshold<16>, dim3(static_cast<unsigned>((nq + 15) / 16)), dim3(256), 0, st,
+                           lists, n_lists, list_stride, nq, rank, thr, top);
     else
-        return RT_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL(flatip_topk_v4_threshold<64>, dim3(static_cast<unsigned>((nq + 3) / 4)), dim3(256), 0, st,
+                           lists, n_lists, list_stride, nq, rank, thr, top);
     return check_launch("flatip_topk_v4_threshold");
 }
 

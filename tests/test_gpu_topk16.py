@@ -263,3 +263,26 @@ def test_shard_global_threshold_emulated(K, V4, n_shards, nx, k):
                                 nthreads=16)
     assert np.array_equal(mi.cpu().numpy()[sel], ri)
     assert np.array_equal(ms.cpu().numpy()[sel], rs)
+
+
+@pytest.mark.parametrize("n_lists", [1, 3, 8, 16, 17, 64])
+@pytest.mark.parametrize("rank", [1, 7, 32])
+def test_sample_threshold_kway_merge(K, n_lists, rank):
+    """rt_topk_sample_threshold's k-way merge (16- and 64-lane groups) equals
+    the rank-th largest of the sorted union: ragged lists (-inf tails), exact
+    ties across lists, empty queries (-FLT_MAX), nq not a multiple of the
+    block's query count."""
+    g = torch.Generator().manual_seed(100 * n_lists + rank)
+    nq = 1001
+    vals = torch.randint(-20, 21, (n_lists, nq, 32), generator=g).float() / 4
+    fill = torch.randint(0, 33, (n_lists, nq), generator=g)
+    fill[:, 5] = 0  # query 5: every list empty
+    mask = torch.arange(32).view(1, 1, 32) >= fill.unsqueeze(2)
+    vals = vals.masked_fill(mask, float("-inf"))
+    lists = vals.sort(dim=2, descending=True).values
+    union = lists.permute(1, 0, 2).reshape(nq, -1).sort(dim=1, descending=True).values
+    want = union[:, rank - 1].clamp(min=-torch.finfo(torch.float32).max)
+    thr = K.topk_sample_threshold(lists.cuda(), rank)
+    torch.cuda.synchronize()
+    assert torch.equal(thr.cpu(), want)
+    assert thr[5].item() == -torch.finfo(torch.float32).max
