@@ -22,6 +22,9 @@ for f in $T/csrc/*.hip; do
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p || { echo "compile failed"; exit 1; }; done
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT.tmp $T/obj/*.o && mv -f $OUT.tmp $OUT
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT.tmp $T/obj/*.o
+# a kernel template whose host pass failed leaves its launch stub undefined
+if nm -C $OUT.tmp | grep -q " U .*__device_stub__"; then echo "undefined kernel stubs in $OUT"; exit 1; fi
+mv -f $OUT.tmp $OUT
 rm -rf $T
 echo built $OUT
