@@ -154,11 +154,7 @@ template <int DP, int PASS> struct Geo {
     static constexpr int WAVES = (PASS != 0 && DP > 128) ? 4 : 8;
     // streamed rows per LDS stage: 128 for the one-wave-per-SIMD gradient passes
     // (4 sub-tiles to pipeline over), 64 where two waves per SIMD share the registers
-#ifdef IB16_LSE_NT128
     static constexpr int NT = (DP > 128) ? 128 : 64;
-#else
-    static constexpr int NT = (PASS != 0 && DP > 128) ? 128 : 64;
-#endif
     static constexpr int SUB = NT / 32;                 // 32-row sub-tiles per stage
     static constexpr int DB = DP / 32;                  // 32-wide d blocks of the gradient
     static constexpr int FT = 32 * WAVES;               // fixed rows per block
@@ -250,13 +246,6 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             if (wave == 0 && lane < NT / 4) glds16(a.lse2 + t0 + 4 * lane, lds_addr(&tlse[buf][0]));
         }
     };
-#ifdef IB16_DMA_SPREAD
-    // one 1-KiB piece j of a full stage at t0 (rows and lse2 of a full stage
-    // only: fetch() covers the others), issued where the scheduler can place it
-    auto fetch_piece = [&](int64_t t0, int buf, int j) {
-        glds16_s(X + t0 * d, voff[j], lds_addr(&tile[buf][0]) + wave_u * (DPW * 1024) + j * 1024);
-    };
-#endif
     auto raw_barrier = [&]() {
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
@@ -303,40 +292,6 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
         return (dl >= 0 && dl < 32 ? static_cast<int>(dl) : 64) - 4 * h;
     };
     // LSE: online base-2 log-sum-exp over the sub-tile's valid rows (left of 32)
-#ifdef IB16_LSE2
-    // wave-uniform: the wave's 32 label items [lab0, lab0 + 32) meet this sub-tile
-    const int64_t lab0 = fblk * G::FT + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(wave)) * 32 + a.off;
-    auto lse_update = [&](const f32x16& acc, int64_t sub0, int left) {
-        const int lim = left - 4 * h;
-        float y[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) y[r] = acc[r];
-        if (left < 32) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-                if (krow(r) >= lim) y[r] = -INFINITY;
-        }
-        // max over the raw products (c2 > 0), then one fma per exp argument
-        float mx = fmaxf(fmaxf(y[0], y[1]), y[2]);
-#pragma unroll
-        for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, y[r]), y[r + 1]);
-        mx = fmaxf(mx, y[15]);
-        const float mn = fmaxf(run_m, mx * a.c2);
-        float s = (mn == -INFINITY) ? 0.f : run_s * __builtin_amdgcn_exp2f(run_m - mn);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s += __builtin_amdgcn_exp2f(__builtin_fmaf(y[r], a.c2, -mn));
-        run_m = mn;
-        run_s = s;
-        if (lab0 + 32 > sub0 && lab0 < sub0 + 32) {  // wave-uniform
-            const int lr = lab_pos(sub0);
-            if (fok && static_cast<unsigned>(lr) < 28u) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (krow(r) == lr) dg = acc[r] * a.c2;
-            }
-        }
-    };
-#else
     auto lse_update = [&](const f32x16& acc, int64_t sub0, int left) {
         const int lim = left - 4 * h;  // row krow(r) + 4h is valid <=> krow(r) < lim
         float x[16];
@@ -365,7 +320,6 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
                 if (krow(r) == lr) dg = x[r];
         }
     };
-#endif
     // ROW/COL: the softmax part of dS, 2^(x − lse2_user)·kScale, in registers as
     // 16-bit hi + lo (the label term −[label] is applied by the reduce launch)
     auto make_ds = [&](const f32x16& acc, const float* tls, int rt, int64_t sub0, int left, s16x8 (&bh)[2],
@@ -441,121 +395,12 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             acc = acc_n;
         }
     };
-#ifdef IB16_MANUAL
-    // gradient passes, issue order fixed by hand (every step fenced by a
-    // sched_barrier): per sub-tile rt, 16 steps of {S MFMA of rt+1, the
-    // exp/split VALU of one dS element of rt, the S fragment read of rt+2}
-    // then 4·DB steps of {gradient MFMA of rt, a transposed read of rt+1};
-    // every read lands a phase before its consumer
-    auto stage_full_m = [&](int64_t t0, const char* tl, const float* tls) {
-        s16x8 af[S16];
-        load_s(tl, 0, af);
-        f32x16 acc = mma_s(af);
-        s16x8 ga[G::DB][2];
-        load_g(tl, 0, ga);
-        if (G::SUB > 1) load_s(tl, 1, af);
-        __builtin_amdgcn_sched_barrier(0);
-        const int g16 = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-#pragma unroll
-        for (int rt = 0; rt < G::SUB; ++rt) {
-            float lrow[16];
-            if constexpr (PASS == COL) {
-                const float* t = tls + rt * 32;
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float4 v = *reinterpret_cast<const float4*>(t + 8 * g + 4 * h);
-                    lrow[4 * g] = v.x - Split<T>::kLog2Scale; lrow[4 * g + 1] = v.y - Split<T>::kLog2Scale;
-                    lrow[4 * g + 2] = v.z - Split<T>::kLog2Scale; lrow[4 * g + 3] = v.w - Split<T>::kLog2Scale;
-                }
-            }
-            f32x16 acc_n = {};
-#ifdef IB16_S2ACC
-            f32x16 acc_o = {};  // odd k-steps: two independent chains
-#endif
-            float ds[16];
-            uint32_t hp[8], lp[8];
-            const int row2 = (rt + 2) * 32 + col;
-#pragma unroll
-            for (int ss = 0; ss < S16; ++ss) {
-#ifdef IB16_S2ACC
-                if (rt + 1 < G::SUB) {
-                    if (ss & 1) acc_o = MM::run(af[ss], qf[ss], acc_o);
-                    else acc_n = MM::run(af[ss], qf[ss], acc_n);
-                }
-#else
-                if (rt + 1 < G::SUB) acc_n = MM::run(af[ss], qf[ss], acc_n);
-#endif
-                // the 16 dS elements spread over the S16 steps
-#pragma unroll
-                for (int e = ss * 16 / S16; e < (ss + 1) * 16 / S16; ++e) {
-                    const float l = (PASS == ROW) ? lse_f : lrow[e];
-#ifdef IB16_T_NOEXP  // timing-only bound
-                    ds[e] = acc[e] * a.c2 - l;
-#else
-                    ds[e] = __builtin_amdgcn_exp2f(acc[e] * a.c2 - l);
-#endif
-                    if (e & 1) Split<T>::run(ds[e - 1], ds[e], hp[e >> 1], lp[e >> 1]);
-                }
-                if (rt + 2 < G::SUB) {
-                    const int cg = 2 * ss + h;
-                    af[ss] = __builtin_bit_cast(s16x8, *reinterpret_cast<const uint4*>(
-                                                           tl + img_off<NT>(cg >> 4, row2, cg & 15)));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            s16x8 bh[2], bl[2];
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                bh[s2] = __builtin_bit_cast(s16x8, make_uint4(hp[4 * s2], hp[4 * s2 + 1], hp[4 * s2 + 2], hp[4 * s2 + 3]));
-                bl[s2] = __builtin_bit_cast(s16x8, make_uint4(lp[4 * s2], lp[4 * s2 + 1], lp[4 * s2 + 2], lp[4 * s2 + 3]));
-            }
-#ifdef IB16_ILV
-            // hi products of every d block first, then the lo ones: consecutive
-            // MFMAs never share an accumulator
-#pragma unroll
-            for (int db = 0; db < G::DB; ++db) {
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    gacc[db] = MM::run(ga[db][s2], bh[s2], gacc[db]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-#endif
-#pragma unroll
-            for (int db = 0; db < G::DB; ++db) {
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-#ifndef IB16_ILV
-                    gacc[db] = MM::run(ga[db][s2], bh[s2], gacc[db]);
-#endif
-#ifndef IB16_T_NOLO  // timing-only bound: the hi half of dS only
-                    gacc[db] = MM::run(ga[db][s2], bl[s2], gacc[db]);
-#endif
-                    if (rt + 1 < G::SUB) {
-                        const int half = db >> 2;
-                        const int c0 = ((db & 3) * 32 + 16 * (g16 & 1)) >> 3;
-                        const int r0 = (rt + 1) * 32 + 16 * s2 + 4 * h;
-                        const s16x4 lo4 = tr_read(tl, img_off<NT>(half, r0 + q4, c0 + (p4 >> 1)) + 8 * (p4 & 1));
-                        const s16x4 hi4 = tr_read(tl, img_off<NT>(half, r0 + 8 + q4, c0 + (p4 >> 1)) + 8 * (p4 & 1));
-                        ga[db][s2] = s16x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-#ifdef IB16_S2ACC
-            acc_n += acc_o;
-#endif
-            acc = acc_n;
-        }
-    };
-#endif
-#ifdef IB16_PIPE2
     // gradient passes, reads one sub-tile ahead, in place, and an explicit
     // issue pattern: once an S MFMA of rt+1 is issued its fragment registers
     // take a read of rt+2, once a gradient MFMA of rt is issued its transposed
     // fragment takes a read of rt+1, and the dS VALU of rt is spread over the
     // S MFMAs (5 per gap) — no read is waited for by the MFMA right after it
-    auto stage_full_g = [&](int64_t t0, const char* tl, const float* tls, int64_t nt0, int nbuf) {
+    auto stage_full_g = [&](int64_t t0, const char* tl, const float* tls) {
         s16x8 af[S16];
         load_s(tl, 0, af);
         f32x16 acc = mma_s(af);
@@ -580,15 +425,6 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
                                                            tl + img_off<NT>(cg >> 4, row, cg & 15)));
                 }
             }
-#ifdef IB16_DMA_SPREAD
-            // the next stage's pieces over the first SUB-1 sub-tiles (the last
-            // one's MFMAs cover their flight before the stage barrier)
-            constexpr int PER = (DPW + G::SUB - 2) / (G::SUB - 1);
-            if (nt0 >= 0 && rt < G::SUB - 1) {
-#pragma unroll
-                for (int j = rt * PER; j < (rt + 1) * PER && j < DPW; ++j) fetch_piece(nt0, nbuf, j);
-            }
-#endif
             s16x8 bh[2], bl[2];
             make_ds(acc, tls, rt, sub0, 32, bh, bl);
             mma_g(ga, bh, bl);
@@ -609,7 +445,6 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             acc = acc_n;
         }
     };
-#endif
     // the split's last, partial stage: sub-tile by sub-tile with row masks
     auto stage_tail = [&](int64_t t0, const char* tl, const float* tls) {
 #pragma unroll
@@ -640,33 +475,9 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
     const int64_t t_full = i_begin + (i_end - i_begin) / NT * NT;  // end of the full stages
     int64_t t0 = i_begin;
     for (; t0 < t_full; t0 += NT) {
-#ifdef IB16_MANUAL
-        if constexpr (PASS != LSE) {
-#ifndef IB16_T_NODMA  // timing-only bound: stages after the first reuse stale LDS
-            if (t0 + NT < i_end) fetch(t0 + NT, cur ^ 1);
-#endif
-            stage_full_m(t0, tile[cur], tlse[cur]);
-        } else
-#elif defined(IB16_PIPE2)
-        if constexpr (PASS != LSE) {
-            int64_t nt0 = -1;
-#ifdef IB16_DMA_SPREAD
-            // the next stage is a full, in-bounds one: its row pieces go inside the stage
-            if (full_rows && t0 + 2 * NT <= i_end && t0 + 2 * NT <= a.n_stream) nt0 = t0 + NT;
-#endif
-            if (t0 + NT < i_end) {
-                if (nt0 < 0) fetch(t0 + NT, cur ^ 1);
-                else if constexpr (PASS == COL) {
-                    if (wave == 0 && lane < NT / 4) glds16(a.lse2 + nt0 + 4 * lane, lds_addr(&tlse[cur ^ 1][0]));
-                }
-            }
-            stage_full_g(t0, tile[cur], tlse[cur], nt0, cur ^ 1);
-        } else
-#endif
-        {
-            if (t0 + NT < i_end) fetch(t0 + NT, cur ^ 1);
-            stage_full(t0, tile[cur], tlse[cur]);
-        }
+        if (t0 + NT < i_end) fetch(t0 + NT, cur ^ 1);
+        if constexpr (PASS != LSE) stage_full_g(t0, tile[cur], tlse[cur]);
+        else stage_full(t0, tile[cur], tlse[cur]);
         raw_barrier();
         cur ^= 1;
     }
