@@ -56,7 +56,18 @@ def main():
     ap.add_argument("--title", default="rocprofv3 --kernel-trace summary")
     ap.add_argument("--by-grid", action="store_true", help="one row per (kernel, grid size) = per launch shape")
     ap.add_argument("--by-base", action="store_true", help="one row per kernel family (all template instances)")
+    ap.add_argument("--seq", type=int, default=0, help="instead: the last SEQ dispatches in start order (.db only)")
     a = ap.parse_args()
+    if a.seq:
+        c = sqlite3.connect(a.src)
+        cols = [d[0] for d in c.execute("select * from kernels limit 1").description]
+        order = "start" if "start" in cols else "rowid"
+        gx = [g for g in cols if g.lower() in ("grid_x", "grid_size_x", "grid_size")][:1]
+        q = f"select name, duration{', ' + gx[0] if gx else ''} from kernels order by {order}"
+        rows = c.execute(q).fetchall()[-a.seq:]
+        for r in rows:
+            print(f"{r[1] / 1e3:10.1f} us  {r[0].split('(')[0][:90]}  {('grid ' + str(r[2])) if gx else ''}")
+        return
     rows = from_db(a.src, a.by_grid, a.by_base) if a.src.endswith(".db") else from_csv(a.src, a.by_grid, a.by_base)
     agg = defaultdict(list)
     for name, dur in rows:
