@@ -57,8 +57,17 @@ def dist_setup(n_gpus):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # rehearsal knobs for a one-GPU box (never set by the driver): every rank
+        # on cuda:0 (RCCL refuses two ranks on one device, so collectives then
+        # go through gloo)
+        if os.environ.get("RTREC_BENCH_SAME_GPU") == "1":
+            local = 0
+        backend = os.environ.get("RTREC_BENCH_BACKEND", "nccl")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         return dist, rank, world, torch.device("cuda", local)
     return None, 0, 1, torch.device("cuda", 0)
 
