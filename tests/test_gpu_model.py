@@ -347,9 +347,12 @@ def test_cpu_tensors_raise():
 
 def test_tower_forward_is_fp32_class(dev):
     """The tower kernels take fp32 products on the bf16 MFMA (three-piece split,
-    DESIGN.md §5 note i). Against a float64 evaluation of the same module, the
-    device output must be as accurate as torch's own fp32 CPU forward (k = 256
-    and 128 reductions, eval BatchNorm, ReLU, final L2 normalise)."""
+    DESIGN.md §5 note i). Against a float64 evaluation of the same module
+    (k = 256 and 128 reductions, eval BatchNorm, ReLU, final L2 normalise), the
+    device output's max error must stay within 4x the max error of torch's own
+    fp32 CPU forward and below 2e-6 absolute: fp32-class, not bit-compatible —
+    the split drops three piece products of order <= 2^-23 and the MFMA's
+    blocked summation order differs from torch's."""
     import copy
     UserTower, _, _, _ = _mods()
     torch.manual_seed(7)
