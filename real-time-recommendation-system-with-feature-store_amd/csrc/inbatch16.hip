@@ -106,6 +106,7 @@ template <typename T> struct Split;
 template <> struct Split<__hip_bfloat16> {
     static constexpr float kScale = 1.f;  // bf16 keeps the fp32 exponent range
     static constexpr float kLog2Scale = 0.f;
+    static constexpr float kLog2ScaleF = 0.f;  // ROWF: softmax weights up to 2^kSlack
     __device__ static void run(float x0, float x1, uint32_t& hp, uint32_t& lp) {
         typedef __bf16 b2 __attribute__((ext_vector_type(2)));
         const uint32_t hv = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{x0, x1}, b2));
@@ -118,6 +119,9 @@ template <> struct Split<__hip_bfloat16> {
 template <> struct Split<__half> {
     static constexpr float kScale = 32768.f;  // dS·2^15 keeps small probabilities out of f16 underflow
     static constexpr float kLog2Scale = 15.f;
+    // ROWF: weights up to 2^kSlack (lazy reference max), so 2^7 keeps them below
+    // the f16 maximum; weights under 2^-31 of the reference underflow
+    static constexpr float kLog2ScaleF = 7.f;
     __device__ static void run(float x0, float x1, uint32_t& hp, uint32_t& lp) {
         typedef _Float16 h2 __attribute__((ext_vector_type(2)));
         const h2 hv = __builtin_convertvector(f32x2{x0, x1}, h2);
@@ -128,7 +132,10 @@ template <> struct Split<__half> {
     }
 };
 
-enum Pass { LSE = 0, ROW = 1, COL = 2 };
+enum Pass { LSE = 0, ROW = 1, COL = 2, ROWF = 3 };
+// ROWF (LSE and ROW in one pass, online softmax): the exponent reference is
+// raised only when a sub-tile's max exceeds it by more than kSlack (base 2)
+constexpr float kSlack = 8.f;
 
 struct Args {
     const void* fixed;    // rows held as B operand (users for LSE/ROW, items for COL)
@@ -142,9 +149,10 @@ struct Args {
     int splits;
     int64_t per_split;    // streamed rows per split (multiple of NT)
     float2* part;         // LSE: [splits][n_fixed] (max2, sum) base 2
-    float* diag2;         // LSE: [n_fixed] x_ii (base-2 logit of the label)
+    float* diag2;         // LSE / ROWF: [n_fixed] x_ii (base-2 logit of the label)
     const float* lse2;    // ROW/COL: [b] base-2 log-sum-exp per user
-    float* gpart;         // ROW/COL: [splits][n_fixed][DP] gradient partials
+    float* gpart;         // ROW/COL/ROWF: [splits][n_fixed][DP] gradient partials
+                          // (ROWF: weighted by 2^(x - m_split), m_split in part[].x)
 };
 
 template <int DP, int PASS> struct Geo {
@@ -206,27 +214,31 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
     // dS scale folded into the exponent; a padding lane (fixed row past the end)
     // only feeds its own, never stored, gradient column, so it needs no mask
     if constexpr (PASS == ROW) lse_f = (fok ? a.lse2[f] : 0.f) - Split<T>::kLog2Scale;
-    const int64_t lab_row = f + a.off;  // LSE: the item that is this user's label
+    // ROWF: run_m is the exponent reference (shared by the two lane halves of a
+    // fixed row), run_s this half's sum of 2^(x - run_m)·2^kLog2ScaleF
+    const int64_t lab_row = f + a.off;  // LSE / ROWF: the item that is this user's label
+    // wave-uniform: the wave's 32 label items are [lab0, lab0 + 32)
+    const int64_t lab0 = fblk * G::FT + static_cast<int64_t>(__builtin_amdgcn_readfirstlane(wave)) * 32 + a.off;
 
     // ---- LDS-DMA of one stage: 1 KiB per wave-instruction into the lane-linear image ----
     const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
     const bool full_rows = (d == DP);  // no zero-filled columns: fixed per-lane offsets
-    uint32_t voff[DPW];                // this lane's byte offset from the stage's first row
-#pragma unroll
-    for (int j = 0; j < DPW; ++j) {
+    // this lane's byte offset of DMA piece j from the stage's first row
+    // (recomputed per stage: the gradient passes have no registers to keep 16)
+    auto voff = [&](int j) {
         const int o = (wave * DPW + j) * 1024 + lane * 16;
         const int half = o / (NT * 256);
         const int oo = o - half * (NT * 256);
         const int r = oo >> 8;
         const int c = half * 16 + (((oo & 255) >> 4) ^ swz(r));
-        voff[j] = static_cast<uint32_t>(r * d * 2 + c * 16);
-    }
+        return static_cast<uint32_t>(r * d * 2 + c * 16);
+    };
     auto fetch = [&](int64_t t0, int buf) {
         const uint32_t base = lds_addr(&tile[buf][0]) + wave_u * (DPW * 1024);
         if (full_rows && t0 + NT <= a.n_stream) {
             const void* sb = X + t0 * d;
 #pragma unroll
-            for (int j = 0; j < DPW; ++j) glds16_s(sb, voff[j], base + j * 1024);
+            for (int j = 0; j < DPW; ++j) glds16_s(sb, voff(j), base + j * 1024);
         } else {  // zero-filled columns past d and/or rows clamped at the split end
 #pragma unroll
             for (int j = 0; j < DPW; ++j) {
@@ -320,6 +332,45 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
                 if (krow(r) == lr) dg = x[r];
         }
     };
+    // ROWF: the sub-tile's max per fixed row (both lane halves), the lazy
+    // reference raise with its rescale of the accumulators (wave-uniform
+    // branch, taken on a wave's first sub-tiles and rarely after), the label logit
+    auto rowf_prep = [&](const f32x16& acc, int64_t sub0, int left) {
+        const int lim = left - 4 * h;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (left >= 32 || krow(r) < lim) mx = fmaxf(mx, acc[r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * a.c2;  // c2 > 0
+        const bool up = mx > run_m + kSlack;
+        if (__builtin_expect(__ballot(up) != 0ull, 0)) {
+            asm volatile("; ib16 rowf rescale" ::: "memory");  // a real branch: never if-converted
+            const float fct = up ? __builtin_amdgcn_exp2f(run_m - mx) : 1.f;  // 0 from -inf
+            // the accumulators stay in AGPRs: each element is read, scaled and
+            // written back through one VGPR (a VALU multiply on the vector
+            // would make the allocator move all 128 of them into VGPRs)
+#pragma unroll
+            for (int db = 0; db < G::DB; ++db)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    float v = gacc[db][r], t;
+                    asm volatile("v_accvgpr_read_b32 %0, %1\n\tv_mul_f32 %0, %0, %2\n\tv_accvgpr_write_b32 %1, %0"
+                                 : "=&v"(t), "+a"(v)
+                                 : "v"(fct));
+                    gacc[db][r] = v;
+                }
+            run_s *= fct;
+            run_m = up ? mx : run_m;
+        }
+        if (lab0 + 32 > sub0 && lab0 < sub0 + 32) {  // wave-uniform
+            const int lr = lab_pos(sub0);
+            if (fok && static_cast<unsigned>(lr) < 28u) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (krow(r) == lr) dg = acc[r] * a.c2;
+            }
+        }
+    };
     // ROW/COL: the softmax part of dS, 2^(x − lse2_user)·kScale, in registers as
     // 16-bit hi + lo (the label term −[label] is applied by the reduce launch)
     auto make_ds = [&](const f32x16& acc, const float* tls, int rt, int64_t sub0, int left, s16x8 (&bh)[2],
@@ -334,16 +385,28 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             }
         }
         float ds[16];
+        if constexpr (PASS == ROWF) {  // 2^(x − run_m)·2^kLog2ScaleF, summed into run_s
+            const float l = run_m - Split<T>::kLog2ScaleF;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float l = (PASS == ROW) ? lse_f : lse_r[r] - Split<T>::kLog2Scale;
-            ds[r] = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
+            for (int r = 0; r < 16; ++r) ds[r] = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float l = (PASS == ROW) ? lse_f : lse_r[r] - Split<T>::kLog2Scale;
+                ds[r] = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
+            }
         }
         if (left < 32) {
             const int lim = left - 4 * h;
 #pragma unroll
             for (int r = 0; r < 16; ++r)
                 if (krow(r) >= lim) ds[r] = 0.f;
+        }
+        if constexpr (PASS == ROWF) {
+            float t = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t += ds[r];
+            run_s += t;
         }
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
@@ -411,6 +474,10 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
 #pragma unroll
         for (int rt = 0; rt < G::SUB; ++rt) {
             const int64_t sub0 = t0 + rt * 32;
+            if constexpr (PASS == ROWF) {
+                rowf_prep(acc, sub0, 32);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             f32x16 acc_n = {};
             if (rt + 1 < G::SUB) {
 #pragma unroll
@@ -460,6 +527,7 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             } else {
                 s16x8 ga[G::DB][2];
                 load_g(tl, rt, ga);
+                if constexpr (PASS == ROWF) rowf_prep(acc, sub0, left);
                 s16x8 bh[2], bl[2];
                 make_ds(acc, tls, rt, sub0, left, bh, bl);
                 mma_g(ga, bh, bl);
@@ -499,9 +567,23 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             }
         }
     } else {
+        if constexpr (PASS == ROWF) {  // the split's (reference, Σ 2^(x − reference)) and label logit
+            const float sc = exp2f(-Split<T>::kLog2ScaleF);
+            const float s_all = (run_s + __shfl_xor(run_s, 32, 64)) * sc;
+            const float dgo = __shfl_xor(dg, 32, 64);
+            if (fok && h == 0) {
+                a.part[static_cast<int64_t>(split) * a.n_fixed + f] = make_float2(run_m, s_all);
+                const int64_t lab = f + a.off;
+                if (lab >= i_begin && lab < i_end) {
+                    const int64_t rr = lab - (i_begin + ((lab - i_begin) & ~31ll));
+                    a.diag2[f] = ((rr >> 2) & 1) ? dgo : dg;
+                }
+            }
+        }
         // gaccᵀ[db][r] = grad[d = 32db + krow(r) + 4h][fixed row f] → partial [split][f][DP]
         if (fok) {
-            const float gs = a.inv_tau * a.w / Split<T>::kScale;
+            const float gs = a.inv_tau * a.w /
+                             (PASS == ROWF ? exp2f(Split<T>::kLog2ScaleF) : Split<T>::kScale);
             float* gp = a.gpart + (static_cast<int64_t>(split) * a.n_fixed + f) * DP;
 #pragma unroll
             for (int db = 0; db < G::DB; ++db)
@@ -543,20 +625,30 @@ __global__ __launch_bounds__(256) void ib16_finalize_kernel(const float2* __rest
     }
 }
 
-// out[r][c] = Σ_s part[s][r][c] (fixed order) − coef·lab[r + lab_off][c] (the
-// label term of dS = softmax − I, when row r + lab_off of lab exists), c < d
+// out[r][c] = Σ_s wt_s·part[s][r][c] (fixed order) − coef·lab[r + lab_off][c]
+// (the label term of dS = softmax − I, when row r + lab_off of lab exists),
+// c < d; wt_s = 1, or with ROWF partials (ml non-NULL) 2^(ml[s][r].x − lse2[r]),
+// the split's exponent reference over the row's log-sum-exp
 template <typename T>
 __global__ __launch_bounds__(256) void ib16_reduce_kernel(const float* __restrict__ part, int splits, int64_t rows,
                                                           int dp, int d, const T* __restrict__ lab, int64_t lab_off,
-                                                          int64_t lab_rows, float coef, float* __restrict__ out) {
+                                                          int64_t lab_rows, float coef, float* __restrict__ out,
+                                                          const float2* __restrict__ ml,
+                                                          const float* __restrict__ lse2) {
     const int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * 4;
     const int64_t total = rows * d;
     if (e >= total) return;
     const int64_t r = e / d;
     const int c = static_cast<int>(e - r * d);
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float l2 = ml ? lse2[r] : 0.f;
     for (int s = 0; s < splits; ++s) {
-        const float4 v = *reinterpret_cast<const float4*>(part + (static_cast<int64_t>(s) * rows + r) * dp + c);
+        float4 v = *reinterpret_cast<const float4*>(part + (static_cast<int64_t>(s) * rows + r) * dp + c);
+        if (ml) {
+            const float m = ml[static_cast<int64_t>(s) * rows + r].x;
+            const float wt = m == -INFINITY ? 0.f : exp2f(m - l2);
+            v.x *= wt; v.y *= wt; v.z *= wt; v.w *= wt;
+        }
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
     const int64_t lr = r + lab_off;
@@ -604,11 +696,12 @@ inline Plan make_plan_t(int64_t b, int64_t nx) {
     Plan p{};
     p.dp = DP;
     p.lse = pass_plan(b, nx, Geo<DP, LSE>::FT, Geo<DP, LSE>::NT);
-    p.row = pass_plan(b, nx, Geo<DP, ROW>::FT, Geo<DP, ROW>::NT);
+    p.row = pass_plan(b, nx, Geo<DP, ROWF>::FT, Geo<DP, ROWF>::NT);
     p.col = pass_plan(nx, b, Geo<DP, COL>::FT, Geo<DP, COL>::NT);
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     size_t o = 0;
-    p.part_off = o; o += al(static_cast<size_t>(p.lse.splits) * b * sizeof(float2));
+    const int part_splits = p.lse.splits > p.row.splits ? p.lse.splits : p.row.splits;  // LSE or ROWF partials
+    p.part_off = o; o += al(static_cast<size_t>(part_splits) * b * sizeof(float2));
     p.diag_off = o; o += al(static_cast<size_t>(b) * sizeof(float));
     // the COL pass DMAs NT lse2 values per stage: padded past b by a whole stage
     p.lse_off = o; o += al(static_cast<size_t>((b + 255) / 256 * 256 + 256) * sizeof(float));
@@ -644,25 +737,30 @@ static int ib16_run_t(const void* u, const void* p, int64_t b, int64_t nx, int d
     float* lse2 = reinterpret_cast<float*>(ws + pl.lse_off);
     a.lse2 = lse2;
     a.gpart = reinterpret_cast<float*>(ws + pl.gp_off);
-    const dim3 blk_l(Geo<DP, LSE>::WAVES * 64), blk_r(Geo<DP, ROW>::WAVES * 64), blk_c(Geo<DP, COL>::WAVES * 64);
+    const dim3 blk_l(Geo<DP, LSE>::WAVES * 64), blk_r(Geo<DP, ROWF>::WAVES * 64), blk_c(Geo<DP, COL>::WAVES * 64);
     auto grid = [](const PassPlan& q) { return dim3(static_cast<unsigned>(q.fixed_blocks * q.splits)); };
-    // lse
     a.fixed = u; a.stream = p; a.n_fixed = b; a.n_stream = nx;
-    a.splits = pl.lse.splits; a.per_split = pl.lse.per;
-    hipLaunchKernelGGL((ib16_kernel<T, DP, LSE>), grid(pl.lse), blk_l, 0, st, a);
-    int rc = check_launch("ib16_kernel<lse>");
-    if (rc) return rc;
-    hipLaunchKernelGGL(ib16_finalize_kernel, dim3(static_cast<unsigned>((b + 255) / 256)), dim3(256), 0, st, a.part,
-                       pl.lse.splits, b, a.diag2, lse2, loss_out);
-    if ((rc = check_launch("ib16_finalize_kernel"))) return rc;
-    if (!du) return RT_OK;
-    // row pass: dU
-    a.splits = pl.row.splits; a.per_split = pl.row.per;
-    hipLaunchKernelGGL((ib16_kernel<T, DP, ROW>), grid(pl.row), blk_r, 0, st, a);
-    if ((rc = check_launch("ib16_kernel<row>"))) return rc;
+    int rc;
     const float coef = inv_tau * a.w;  // d L/d S_label = −w, times 1/τ
+    if (!du) {  // loss only: the LSE pass
+        a.splits = pl.lse.splits; a.per_split = pl.lse.per;
+        hipLaunchKernelGGL((ib16_kernel<T, DP, LSE>), grid(pl.lse), blk_l, 0, st, a);
+        if ((rc = check_launch("ib16_kernel<lse>"))) return rc;
+        hipLaunchKernelGGL(ib16_finalize_kernel, dim3(static_cast<unsigned>((b + 255) / 256)), dim3(256), 0, st,
+                           a.part, pl.lse.splits, b, a.diag2, lse2, loss_out);
+        return check_launch("ib16_finalize_kernel");
+    }
+    // LSE and dU in one pass (online softmax per split), then the row
+    // log-sum-exp, the loss and the split-weighted dU reduce
+    a.splits = pl.row.splits; a.per_split = pl.row.per;
+    hipLaunchKernelGGL((ib16_kernel<T, DP, ROWF>), grid(pl.row), blk_r, 0, st, a);
+    if ((rc = check_launch("ib16_kernel<rowf>"))) return rc;
+    hipLaunchKernelGGL(ib16_finalize_kernel, dim3(static_cast<unsigned>((b + 255) / 256)), dim3(256), 0, st, a.part,
+                       pl.row.splits, b, a.diag2, lse2, loss_out);
+    if ((rc = check_launch("ib16_finalize_kernel"))) return rc;
     hipLaunchKernelGGL(ib16_reduce_kernel<T>, dim3(static_cast<unsigned>((b * d / 4 + 255) / 256)), dim3(256), 0, st,
-                       a.gpart, pl.row.splits, b, DP, d, reinterpret_cast<const T*>(p), off, nx, coef, du);
+                       a.gpart, pl.row.splits, b, DP, d, reinterpret_cast<const T*>(p), off, nx, coef, du,
+                       static_cast<const float2*>(a.part), static_cast<const float*>(lse2));
     if ((rc = check_launch("ib16_reduce_kernel(du)"))) return rc;
     // column pass: dP (items fixed, users streamed)
     a.fixed = p; a.stream = u; a.n_fixed = nx; a.n_stream = b;
@@ -670,7 +768,8 @@ static int ib16_run_t(const void* u, const void* p, int64_t b, int64_t nx, int d
     hipLaunchKernelGGL((ib16_kernel<T, DP, COL>), grid(pl.col), blk_c, 0, st, a);
     if ((rc = check_launch("ib16_kernel<col>"))) return rc;
     hipLaunchKernelGGL(ib16_reduce_kernel<T>, dim3(static_cast<unsigned>((nx * d / 4 + 255) / 256)), dim3(256), 0, st,
-                       a.gpart, pl.col.splits, nx, DP, d, reinterpret_cast<const T*>(u), -off, b, coef, dp);
+                       a.gpart, pl.col.splits, nx, DP, d, reinterpret_cast<const T*>(u), -off, b, coef, dp,
+                       static_cast<const float2*>(nullptr), static_cast<const float*>(nullptr));
     return check_launch("ib16_reduce_kernel(dp)");
 }
 
