@@ -70,3 +70,26 @@ def test_inbatch16_c5_full_size(device):
     np.testing.assert_allclose(loss[0].item(), rl, rtol=1e-4)
     np.testing.assert_allclose(du.cpu().numpy(), rdu, rtol=0, atol=1e-4 * np.abs(rdu).max())
     np.testing.assert_allclose(dp.cpu().numpy(), rdp, rtol=0, atol=1e-4 * np.abs(rdp).max())
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_inbatch16_online_softmax_reference_raises(device, dtype):
+    """The fused LSE + dU pass keeps an exponent reference per (user, item
+    split) and raises it (rescaling the accumulated dU) when a later sub-tile's
+    max exceeds it by more than 2^8. Unnormalized rows whose norms grow along
+    the item axis push every user's max up stage after stage — and the label
+    items (diagonal) of the last quarter dominate — so the raise path runs many
+    times per split; the result must still match the fp32 reference."""
+    g = torch.Generator().manual_seed(11)
+    b, d = 2048, 256
+    U = torch.nn.functional.normalize(torch.randn(b, d, generator=g), dim=1)
+    P = torch.nn.functional.normalize(torch.randn(b, d, generator=g), dim=1)
+    P = P * torch.linspace(0.2, 3.0, b).unsqueeze(1)  # logits grow along the items
+    P[3 * b // 4:] += 2.0 * U[3 * b // 4:]            # late labels far above the rest
+    U, P = U.to(dtype), P.to(dtype)
+    rl, rdu, rdp = _ref(U, P, 0.05)
+    loss, du, dp = kernels.inbatch_loss(U.to(device), P.to(device), 0.05)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss[0].item(), rl, rtol=1e-4)
+    np.testing.assert_allclose(du.cpu().numpy(), rdu, rtol=0, atol=1e-4 * np.abs(rdu).max())
+    np.testing.assert_allclose(dp.cpu().numpy(), rdp, rtol=0, atol=1e-4 * np.abs(rdp).max())
