@@ -219,8 +219,12 @@ class FusedTrainStep:
     def _allreduce(self):
         if self.pg is not None:  # data parallel: average the flat grad slab (one RCCL all-reduce)
             import torch.distributed as dist
-            dist.all_reduce(self.slab.grad, op=dist.ReduceOp.SUM, group=self.pg)
-            self.slab.grad.mul_(1.0 / dist.get_world_size(self.pg))
+            if dist.get_backend(self.pg) == "nccl":
+                # RCCL averages in the collective (ncclAvg): no separate scaling launch
+                dist.all_reduce(self.slab.grad, op=dist.ReduceOp.AVG, group=self.pg)
+            else:  # gloo has no AVG
+                dist.all_reduce(self.slab.grad, op=dist.ReduceOp.SUM, group=self.pg)
+                self.slab.grad.mul_(1.0 / dist.get_world_size(self.pg))
 
     def _update(self):
         """clip_grad_norm_ + Adam on the flat slabs (device step counter / lr)."""

@@ -73,12 +73,14 @@ def test_graph_capture_keeps_warmup_when_asked(device):
     _check(m1, m2, ref[2:], got)
 
 
-def test_two_graph_data_parallel_capture(device):
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_two_graph_data_parallel_capture(device, backend):
     """The data-parallel form bench.py replays at N > 1: with a process group the
     step is captured as two graphs (gradients; clip+Adam) with the all-reduce
     of the flat grad slab launched eagerly between them. Exercised here with a
-    one-rank gloo group (the all-reduce is then x·1): the replays equal the
-    eager single-process steps."""
+    one-rank group (the all-reduce is then the identity): gloo (SUM + scale)
+    and nccl = RCCL (ReduceOp.AVG, the path of the multi-GPU bench); the
+    replays equal the eager single-process steps."""
     import socket
 
     import torch.distributed as dist
@@ -87,7 +89,8 @@ def test_two_graph_data_parallel_capture(device):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    kw = {"device_id": torch.device(device)} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, **kw)
     try:
         ut, mt, batches, m1 = _setup(device)
         m2 = copy.deepcopy(m1)
