@@ -194,20 +194,32 @@ def sharded_topk_global(queries: torch.Tensor, k: int, n_total: int, ops, merge:
         LAST_TOPK.clear()
         LAST_TOPK.update({"path": "plain (no v4 plan on some shard)"})
         return plain(queries, k, ops.topk, merge, group)
-    top = smp[0].contiguous()
-    lists = torch.empty((world * nq, top.shape[1]), dtype=top.dtype, device=dev)
-    dist.all_gather_into_tensor(lists, top, group=group)
-    r = ops.rank(k, sampled, stages)
+    top = smp[0]
+    r = ops.rank(k, sampled, stages)  # the same on every rank (global counts)
     if r > 0:
-        thr = ops.threshold(lists.view(world, nq, top.shape[1]), r)
+        # the rank-th largest of the union needs only each list's top r; every
+        # entry rounded DOWN to bf16 keeps the threshold at or below the exact
+        # one (safe: at most a few more candidates), so r x 2 bytes per query
+        # cross the links instead of 32 x 4
+        # (the 16-bit patterns travel as a float16 view: a type both RCCL and
+        # gloo move, and an all-gather copies bits without arithmetic)
+        mine = _bf16_floor_bits(top[:, :r].contiguous()).view(torch.float16)
+        got = torch.empty((world * nq, r), dtype=torch.float16, device=dev)
+        dist.all_gather_into_tensor(got, mine, group=group)
+        lists = torch.full((world, nq, top.shape[1]), float("-inf"), dtype=torch.float32, device=dev)
+        lists[:, :, :r] = _bf16_bits_to_f32(got.view(torch.int16)).view(world, nq, r)
+        thr = ops.threshold(lists, r)
     else:
         thr = torch.full((nq,), -3.4028234663852886e38, dtype=torch.float32, device=dev)
     s, i = ops.search(queries, k, thr)
     if owner:
-        s, i = s.contiguous(), i.contiguous()
+        s = s.contiguous()
+        # ids cross as int32 when the corpus allows it (-1 padding survives)
+        i = i.to(torch.int32).contiguous() if n_total < 2 ** 31 else i.contiguous()
         out_s, out_i = torch.empty_like(s), torch.empty_like(i)
         dist.all_to_all_single(out_s, s, group=group)
         dist.all_to_all_single(out_i, i, group=group)
+        out_i = out_i.to(torch.int64)
         per = nq // world
         ms, mi = merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
     else:
@@ -239,6 +251,21 @@ def sharded_topk_global(queries: torch.Tensor, k: int, n_total: int, ops, merge:
     LAST_TOPK.update({"path": "global threshold", "stride": stride, "rank": r, "sampled_stages": sampled,
                       "stages": stages, "rescued_queries": n_bad})
     return ms, mi
+
+
+def _bf16_floor_bits(x: torch.Tensor) -> torch.Tensor:
+    """fp32 -> int16 bf16 bit patterns rounded toward -inf (truncation for
+    x >= 0, one more magnitude step for negative x with dropped bits)."""
+    bits = x.contiguous().view(torch.int32)
+    hi = torch.bitwise_right_shift(bits, 16)  # arithmetic: the sign stays
+    bump = (bits < 0) & (torch.bitwise_and(bits, 0xFFFF) != 0)
+    return (hi + bump.to(torch.int32)).to(torch.int16)
+
+
+def _bf16_bits_to_f32(b: torch.Tensor) -> torch.Tensor:
+    """int16 bf16 bit patterns -> the fp32 values they denote (exact)."""
+    wide = torch.bitwise_left_shift(torch.bitwise_and(b.to(torch.int64), 0xFFFF), 16)
+    return wide.to(torch.int32).view(torch.float32)
 
 
 def _exchange_rows(local: torch.Tensor, group) -> torch.Tensor:
