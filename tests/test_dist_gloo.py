@@ -400,3 +400,24 @@ def test_sample_rank_matches_library():
     from rtrec_amd import kernels as K
     for k, s, t in [(100, 122, 7813), (10, 16, 977), (100, 2, 977), (50, 40, 40), (128, 31, 1000)]:
         assert K.topk_sample_rank(k, s, t) == orc.sample_rank(k, s, t), (k, s, t)
+
+
+def test_bf16_floor_bits_round_down():
+    """The sample-list exchange of sharded_topk_global sends bf16 patterns
+    rounded toward -inf: every value comes back <= the original (so the
+    derived threshold can only drop), bf16-representable values exactly,
+    -FLT_MAX as -inf, and the patterns survive a float16 view (the wire type)."""
+    from rtrec_amd.dist.sharded import _bf16_bits_to_f32, _bf16_floor_bits
+    g = torch.Generator().manual_seed(0)
+    fmax = float(np.finfo(np.float32).max)
+    x = torch.cat([torch.randn(20000, generator=g) * 30,
+                   torch.tensor([0.0, -0.0, 1.0, -1.0, float("inf"), float("-inf"), fmax, -fmax, 1e-40, -1e-40])])
+    bits = _bf16_floor_bits(x)
+    y = _bf16_bits_to_f32(bits.view(torch.float16).view(torch.int16))
+    assert bool((y <= x).all())
+    assert float(_bf16_bits_to_f32(_bf16_floor_bits(torch.tensor([-fmax])))[0]) == float("-inf")
+    sel = torch.isfinite(x) & torch.isfinite(y) & (x.abs() > 1e-30)
+    gap = (x - y)[sel] / x[sel].abs()
+    assert float(gap.max()) <= 2.0 ** -7  # one bf16 ulp at most
+    z = torch.randn(1000, generator=g).to(torch.bfloat16).float()
+    assert torch.equal(_bf16_bits_to_f32(_bf16_floor_bits(z)), z)
