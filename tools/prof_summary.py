@@ -63,10 +63,19 @@ def main():
         cols = [d[0] for d in c.execute("select * from kernels limit 1").description]
         order = "start" if "start" in cols else "rowid"
         gx = [g for g in cols if g.lower() in ("grid_x", "grid_size_x", "grid_size")][:1]
-        q = f"select name, duration{', ' + gx[0] if gx else ''} from kernels order by {order}"
+        se = ", start, end" if ("start" in cols and "end" in cols) else ""
+        q = f"select name, duration{', ' + gx[0] if gx else ''}{se} from kernels order by {order}"
         rows = c.execute(q).fetchall()[-a.seq:]
+        prev_end = None
         for r in rows:
-            print(f"{r[1] / 1e3:10.1f} us  {r[0].split('(')[0][:90]}  {('grid ' + str(r[2])) if gx else ''}")
+            gap = ""
+            if se:
+                st, en = r[-2], r[-1]
+                if prev_end is not None:
+                    gap = f"gap {(st - prev_end) / 1e3:7.1f} us  "
+                prev_end = en
+            grid = ("grid " + str(r[2])) if gx else ""
+            print(f"{gap}{r[1] / 1e3:10.1f} us  {r[0].split('(')[0][:90]}  {grid}")
         return
     rows = from_db(a.src, a.by_grid, a.by_base) if a.src.endswith(".db") else from_csv(a.src, a.by_grid, a.by_base)
     agg = defaultdict(list)
