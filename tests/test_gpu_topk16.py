@@ -96,7 +96,8 @@ def test_topk16_exclusion_and_offset(K, dtype):
 @pytest.mark.parametrize("k", [100, 10])
 def test_topk16_c4_shard_properties(K, k):
     """C4 shard shape at full size (65,536 queries x 125,000 fp16 rows; k=100
-    runs the v2 kernel, k=10 the v3 scan): size-independent checks — sorted
+    runs the v4 sampled-threshold pair — presample, threshold, scan, finish —
+    k=10 the v3 scan): size-independent checks — sorted
     (score desc, id asc), ids distinct and in range, scores equal to the fp32
     dot of the returned rows (recomputed on the device), and a 512-query sample
     bit-exact against the oracle."""
