@@ -132,13 +132,16 @@ template <> struct Split<__half> {
     }
 };
 
-enum Pass { LSE = 0, ROW = 1, COL = 2, ROWF = 3 };
-// ROWF (LSE and ROW in one pass, online softmax): the exponent reference is
+// LSE: loss only; ROWF: the row log-sum-exp and dU in one pass (online
+// softmax); COL: dP, against the finished lse2 (value 1 was the round-4 ROW
+// pass, which took lse2 from a preceding LSE pass)
+enum Pass { LSE = 0, COL = 2, ROWF = 3 };
+// ROWF: the exponent reference is
 // raised only when a sub-tile's max exceeds it by more than kSlack (base 2)
 constexpr float kSlack = 8.f;
 
 struct Args {
-    const void* fixed;    // rows held as B operand (users for LSE/ROW, items for COL)
+    const void* fixed;    // rows held as B operand (users for LSE/ROWF, items for COL)
     const void* stream;   // rows streamed through LDS
     int64_t n_fixed, n_stream;
     int d;
@@ -150,8 +153,8 @@ struct Args {
     int64_t per_split;    // streamed rows per split (multiple of NT)
     float2* part;         // LSE: [splits][n_fixed] (max2, sum) base 2
     float* diag2;         // LSE / ROWF: [n_fixed] x_ii (base-2 logit of the label)
-    const float* lse2;    // ROW/COL: [b] base-2 log-sum-exp per user
-    float* gpart;         // ROW/COL/ROWF: [splits][n_fixed][DP] gradient partials
+    const float* lse2;    // COL: [b] base-2 log-sum-exp per user
+    float* gpart;         // COL/ROWF: [splits][n_fixed][DP] gradient partials
                           // (ROWF: weighted by 2^(x - m_split), m_split in part[].x)
 };
 
@@ -205,15 +208,13 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
 
     // per-pass state
     float run_m = -INFINITY, run_s = 0.f, dg = 0.f;  // LSE (base 2), diag
-    float lse_f = 0.f;                                // ROW: the user's lse2
-    f32x16 gacc[G::DB];                               // ROW/COL: gradient tile per 32-col d block
+    f32x16 gacc[G::DB];                               // ROWF/COL: gradient tile per 32-col d block
     if constexpr (PASS != LSE) {
 #pragma unroll
         for (int i = 0; i < G::DB; ++i) gacc[i] = f32x16{};
     }
-    // dS scale folded into the exponent; a padding lane (fixed row past the end)
-    // only feeds its own, never stored, gradient column, so it needs no mask
-    if constexpr (PASS == ROW) lse_f = (fok ? a.lse2[f] : 0.f) - Split<T>::kLog2Scale;
+    // a padding lane (fixed row past the end) only feeds its own, never
+    // stored, gradient column, so it needs no mask
     // ROWF: run_m is the exponent reference (shared by the two lane halves of a
     // fixed row), run_s this half's sum of 2^(x - run_m)·2^kLog2ScaleF
     const int64_t lab_row = f + a.off;  // LSE / ROWF: the item that is this user's label
@@ -371,7 +372,7 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             }
         }
     };
-    // ROW/COL: the softmax part of dS, 2^(x − lse2_user)·kScale, in registers as
+    // ROWF/COL: the softmax part of dS, 2^(x − reference)·scale, in registers as
     // 16-bit hi + lo (the label term −[label] is applied by the reduce launch)
     auto make_ds = [&](const f32x16& acc, const float* tls, int rt, int64_t sub0, int left, s16x8 (&bh)[2],
                        s16x8 (&bl)[2]) {
@@ -392,7 +393,7 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
         } else {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float l = (PASS == ROW) ? lse_f : lse_r[r] - Split<T>::kLog2Scale;
+                const float l = lse_r[r] - Split<T>::kLog2Scale;
                 ds[r] = __builtin_amdgcn_exp2f(acc[r] * a.c2 - l);
             }
         }
@@ -428,9 +429,9 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
             }
     };
 
-    // a full stage, software-pipelined by one sub-tile: the S MFMAs of sub-tile
-    // rt+1 are independent of sub-tile rt's exp/split VALU work and overlap it
-    auto stage_full = [&](int64_t t0, const char* tl, const float* tls) {
+    // LSE: a full stage, software-pipelined by one sub-tile: the S MFMAs of
+    // sub-tile rt+1 are independent of sub-tile rt's exp VALU work and overlap it
+    auto stage_full = [&](int64_t t0, const char* tl) {
         s16x8 af[S16];
         load_s(tl, 0, af);
         f32x16 acc = mma_s(af);
@@ -438,23 +439,11 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
         for (int rt = 0; rt < G::SUB; ++rt) {
             const int64_t sub0 = t0 + rt * 32;
             f32x16 acc_n = {};
-            if constexpr (PASS == LSE) {
-                if (rt + 1 < G::SUB) {
-                    load_s(tl, rt + 1, af);
-                    acc_n = mma_s(af);
-                }
-                lse_update(acc, sub0, 32);
-            } else {
-                s16x8 ga[G::DB][2];
-                load_g(tl, rt, ga);
-                if (rt + 1 < G::SUB) {
-                    load_s(tl, rt + 1, af);
-                    acc_n = mma_s(af);
-                }
-                s16x8 bh[2], bl[2];
-                make_ds(acc, tls, rt, sub0, 32, bh, bl);
-                mma_g(ga, bh, bl);
+            if (rt + 1 < G::SUB) {
+                load_s(tl, rt + 1, af);
+                acc_n = mma_s(af);
             }
+            lse_update(acc, sub0, 32);
             acc = acc_n;
         }
     };
@@ -545,7 +534,7 @@ __global__ __launch_bounds__((Geo<DP, PASS>::WAVES * 64)) void ib16_kernel(Args 
     for (; t0 < t_full; t0 += NT) {
         if (t0 + NT < i_end) fetch(t0 + NT, cur ^ 1);
         if constexpr (PASS != LSE) stage_full_g(t0, tile[cur], tlse[cur]);
-        else stage_full(t0, tile[cur], tlse[cur]);
+        else stage_full(t0, tile[cur]);
         raw_barrier();
         cur ^= 1;
     }
