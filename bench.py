@@ -446,14 +446,22 @@ def pmc_traffic(kernel: str):
 
 
 def topk_c4_scaling(dev, dist, rank, world, reps=3):
-    """C4 scaling leg, run collectively on every rank: a 1M-item f16 corpus
-    (emb 128) row-sharded over the ranks (1M/N rows each), 65,536 queries per
-    launch scanned by every rank against its shard (k=100), the per-slice
-    candidate lists sent to the query owners by one all-to-all, owner merge
-    (rtrec_amd/dist/sharded.py::sharded_topk_owner). Strong scaling (fixed corpus);
+    """C4 scaling leg, run collectively on every rank through the product
+    index (rtrec_amd/serving/retrieval.py::HipShardedFlatIPIndex, the
+    RetrievalEngine type "hip_flat_sharded"): a 1M-item f16 corpus (emb 128)
+    row-sharded over the ranks (1M/N rows each, built rank-locally with
+    build_shard), 65,536 queries per launch, k = 100, owner layout
+    (search_tensors(layout="owner")). At N > 1 each launch is
+    sharded_topk_global: every rank samples its shard, one all-gather of the
+    sample lists' top r entries (bf16) gives one corpus-wide threshold per
+    query, each rank searches its shard against it, one all-to-all sends the
+    per-slice lists to the query owners, owner merge, then a device-summed
+    count of short (rescue) queries read once on the host — the stage counts
+    come from the shard sizes on the host (no collective). At N = 1 the index
+    runs the plain single-GPU search. Strong scaling (fixed corpus);
     time = max over ranks between barriers."""
-    from rtrec_amd import kernels
-    from rtrec_amd.dist.sharded import LAST_TOPK, ShardOps, shard_range, sharded_topk_global
+    from rtrec_amd.dist.sharded import LAST_TOPK, shard_range
+    from rtrec_amd.serving.retrieval import HipShardedFlatIPIndex
     n, d, nq, k = 1_000_000, 128, 65536, 100
     b, c = shard_range(n, world, rank)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -461,11 +469,13 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
     gq = torch.Generator(device=dev).manual_seed(99)
     q = torch.nn.functional.normalize(torch.randn(nq, d, device=dev, generator=gq), dim=1).half()
     grp = dist.group.WORLD if dist is not None else None
+    index = HipShardedFlatIPIndex({"dimension": d, "metric": "inner_product", "storage_dtype": "float16",
+                                   "process_group": grp, "device": str(dev)})
+    index.build_shard(shard, n, prepared=True)
+    del shard
 
-    ops = ShardOps(shard, b)
-
-    def run():  # N > 1: one corpus-wide threshold per query (N = 1: the plain single-GPU search)
-        return sharded_topk_global(q, k, n, ops, kernels.topk_merge, grp, owner=True)
+    def run():
+        return index.search_tensors(q, k, layout="owner", prepared=True)
 
     def sync():
         torch.cuda.synchronize()
@@ -484,12 +494,14 @@ def topk_c4_scaling(dev, dist, rank, world, reps=3):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    del shard, q
+    del index, q
     torch.cuda.empty_cache()
     return {"qps": nq * reps / el, "ms_per_launch": 1e3 * el / reps, "n_gpus": world, "corpus_rows": n,
             "shard_rows": c, "queries_per_launch": nq, "k": k, "dtype": "f16",
-            "exchange": ("sample lists all-gather + stage-count all-reduce, shard search against one corpus-wide "
-                         "threshold per query, all_to_all + owner merge" if world > 1 else "none (N = 1)"),
+            "api": "HipShardedFlatIPIndex.search_tensors(layout='owner') (RetrievalEngine 'hip_flat_sharded')",
+            "exchange": ("sample lists all-gather (bf16 top-r), shard search against one corpus-wide threshold per "
+                         "query, all_to_all + owner merge, rescue-count all-reduce (one host read)"
+                         if world > 1 else "none (N = 1)"),
             "global_threshold": dict(LAST_TOPK) if world > 1 else None,
             "scaling": "strong (fixed 1M-row corpus)"}
 

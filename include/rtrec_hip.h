@@ -99,10 +99,19 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
  * most its k-th score over the WHOLE corpus, and each rank keeps only its
  * rows at or above it — so a query's candidates per shard shrink with the
  * number of shards instead of staying ~k per shard.
- *   rt_flatip_topk_shard_sample: top32 [nq][32] = per query the 32 largest
- *     group maxima (max of 16 rows) over every stride-th 128-row stage of the
- *     shard, sorted descending (-inf padded); stage_counts = {sampled stages,
- *     stages} of this shard.
+ *   rt_flatip_topk_shard_sample: top32 [nq][32] = per query the union of each
+ *     lane half's 16 largest group maxima (max of 16 rows) over every
+ *     stride-th 128-row stage of the shard, merged and sorted descending
+ *     (-inf padded): a subset of the 32 largest sampled group maxima, so a
+ *     threshold taken from it is <= the one the exact 32 would give (safe:
+ *     only more candidates). stage_counts = {sampled stages, stages} of this
+ *     shard.
+ *   rt_flatip_topk_shard_plan: host only (no device work): RT_OK and the
+ *     stage_counts rt_flatip_topk_shard_sample would report for a shard of
+ *     nx rows, or RT_ERR_UNSUPPORTED when the shape has no v4 plan — so every
+ *     rank can derive every shard's counts (and whether the global-threshold
+ *     path applies on all of them) from the shard sizes alone, without a
+ *     collective or a device->host read.
  *   rt_topk_sample_rank: the failure-safe rank (P(threshold > k-th) < 1e-6)
  *     for the sampled fraction sum(sampled) / sum(stages) over all shards
  *     (0 = none fits: search from -inf).
@@ -119,6 +128,7 @@ int rt_flatip_topk(const void* queries, int64_t nq, const void* items, int64_t n
  * workspace (rt_flatip_topk_shard_workspace_bytes, 0 = unsupported) serves
  * both the sample and the search of the same shape. */
 size_t rt_flatip_topk_shard_workspace_bytes(int64_t nq, int64_t nx, int d, int dtype, int k);
+int rt_flatip_topk_shard_plan(int64_t nq, int64_t nx, int d, int dtype, int k, int stride, int64_t* stage_counts);
 int rt_flatip_topk_shard_sample(const void* queries, int64_t nq, const void* items, int64_t nx, int d, int dtype,
                                 int k, int stride, float* top32, int64_t* stage_counts, void* workspace,
                                 size_t workspace_bytes, void* stream);

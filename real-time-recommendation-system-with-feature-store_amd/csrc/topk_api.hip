@@ -435,6 +435,31 @@ extern "C" size_t rt_flatip_topk_shard_workspace_bytes(int64_t nq, int64_t nx, i
     return rc ? 0 : s.need + 256;
 }
 
+namespace rt {
+namespace topk {
+// {sampled stages, stages} of a shard under plan p: every split samples its
+// stages 0, stride, 2·stride, ... (the mode-3 scan of v4_scan)
+inline void shard_stage_counts(const Plan& p, int64_t nx, int stride, int64_t* counts) {
+    constexpr int NT = v4::Cfg4<__half, 8>::NT;
+    const int64_t nst = (nx + NT - 1) / NT, sps = (p.items_per_split + NT - 1) / NT;
+    const int64_t nfull = nst / sps, rem = nst - nfull * sps;
+    counts[0] = nfull * ((sps + stride - 1) / stride) + (rem + stride - 1) / stride;
+    counts[1] = nst;
+}
+}  // namespace topk
+}  // namespace rt
+
+extern "C" int rt_flatip_topk_shard_plan(int64_t nq, int64_t nx, int d, int dtype, int k, int stride,
+                                         int64_t* stage_counts) {
+    if (stride < 1 || !stage_counts) return RT_ERR_INVALID;
+    topk::ShardArgs s{};
+    const int rc = topk::shard_setup(reinterpret_cast<const void*>(16), nq, reinterpret_cast<const void*>(16), nx, d,
+                                     dtype, k, reinterpret_cast<void*>(16), ~size_t(0), s);
+    if (rc) return rc;
+    topk::shard_stage_counts(s.p, nx, stride, stage_counts);
+    return RT_OK;
+}
+
 extern "C" int rt_flatip_topk_shard_sample(const void* queries, int64_t nq, const void* items, int64_t nx, int d,
                                            int dtype, int k, int stride, float* top32, int64_t* stage_counts,
                                            void* workspace, size_t workspace_bytes, void* stream) {
@@ -442,11 +467,7 @@ extern "C" int rt_flatip_topk_shard_sample(const void* queries, int64_t nq, cons
     int rc = topk::shard_setup(queries, nq, items, nx, d, dtype, k, workspace, workspace_bytes, s);
     if (rc) return rc;
     if (stride < 1 || !top32 || !stage_counts) return RT_ERR_INVALID;
-    constexpr int NT = topk::v4::Cfg4<__half, 8>::NT;
-    const int64_t nst = (nx + NT - 1) / NT, sps = (s.p.items_per_split + NT - 1) / NT;
-    const int64_t nfull = nst / sps, rem = nst - nfull * sps;
-    stage_counts[0] = nfull * ((sps + stride - 1) / stride) + (rem + stride - 1) / stride;  // sampled stages
-    stage_counts[1] = nst;
+    topk::shard_stage_counts(s.p, nx, stride, stage_counts);
     hipStream_t st = as_stream(stream);
     topk::Args b = s.a;
     b.lists_out = s.a.v4_lists;

@@ -62,7 +62,7 @@ constexpr int kHalf = kCap / 2;        // per owning lane half
 constexpr int kMaxK = 128;
 constexpr int kList = 16;              // group maxima per lane and query set (sample phase)
 constexpr int kMaxSplits = 16;
-constexpr int kSampleList = 32;       // per query: the 32 largest sampled group maxima (both lane halves)
+constexpr int kSampleList = 32;       // per query: each lane half's 16 largest sampled group maxima, merged
 constexpr int kFinishCap = 128;        // survivors a finish wave sorts at once (2 per lane)
 constexpr int kFinishRegs = 16;        // candidates per lane the finish holds in registers
 #ifndef RT_TOPK_V4_QS
@@ -297,8 +297,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     //   a query derives the same threshold, a lower bound of the query's k-th
     //   over the corpus; no per-split verification (the finish checks the union);
     // mode 2 (rescue): only queries the finish flagged (union < k) run, from -inf.
-    // mode 3 (presample): the sample pass over this block's own split only, its
-    //   32 largest group maxima per query to a.lists_out; no main pass
+    // mode 3 (presample): the sample pass over this block's own split only, per
+    //   query the union of each lane half's 16 largest group maxima (a subset
+    //   of the split's 32 largest: a threshold from it can only be lower, i.e.
+    //   safe) to a.lists_out; no main pass
     //   (flatip_topk_v4_threshold turns the lists of all splits — or of all
     //   ranks' shards — into one threshold per query);
     // mode 4: no sample pass, thr = a.thr_in[query], then the main pass.
@@ -623,7 +625,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             cur = cur == C::RING - 1 ? 0 : cur + 1;
         }
         RT_PT(pc_samp = clock64() - pc_start;)
-        if (mode == 3) {  // presample: the split's 32 largest group maxima per query, sorted
+        if (mode == 3) {  // presample: both lane halves' 16 largest group maxima per query, merged and sorted
 #pragma unroll
             for (int j = 0; j < QS; ++j) {
                 float u[2 * kList];

@@ -127,11 +127,24 @@ def sharded_topk_owner(queries: torch.Tensor, k: int, local_topk: TopkFn, merge:
 
 class ShardOps:
     """Per-rank compute of :func:`sharded_topk_global` over one row shard
-    (``shard`` [rows, d], global row ``begin``), bound to the HIP kernels;
-    tests substitute CPU versions of the same five callables."""
+    (``shard`` [rows, d]) bound to the HIP kernels; tests substitute CPU
+    versions of the same six callables. Result ids are GLOBAL row positions:
+    ``begin + local row`` for a contiguous shard, or ``gpos[local row]`` when
+    the shard's rows are not contiguous in the global order (rows appended by
+    ``HipShardedFlatIPIndex.add``). ``gpos`` must be increasing, so the lower
+    local row is the lower global id and the kernels' tie rule (lower id wins)
+    carries over."""
 
-    def __init__(self, shard: torch.Tensor, begin: int):
-        self.shard, self.begin = shard, int(begin)
+    def __init__(self, shard: torch.Tensor, begin: int = 0, gpos: Optional[torch.Tensor] = None):
+        self.shard, self.begin, self.gpos = shard, int(begin), gpos
+
+    def _glob(self, s, i):
+        if self.gpos is None:
+            return s, i
+        return s, torch.where(i >= 0, self.gpos[i.clamp(min=0)], i)
+
+    def plan(self, nq, rows, k, stride):
+        return kernels.flatip_topk_shard_plan(nq, rows, self.shard.shape[1], self.shard.dtype, k, stride)
 
     def sample(self, q, k, stride):
         return kernels.flatip_topk_shard_sample(q, self.shard, k, stride)
@@ -143,58 +156,94 @@ class ShardOps:
         return kernels.topk_sample_threshold(lists, rank)
 
     def search(self, q, k, thr):
-        return kernels.flatip_topk_shard_search(q, self.shard, k, thr, id_offset=self.begin)
+        off = self.begin if self.gpos is None else 0
+        return self._glob(*kernels.flatip_topk_shard_search(q, self.shard, k, thr, id_offset=off))
 
     def topk(self, q, k):
-        return kernels.flatip_topk(q, self.shard, k, id_offset=self.begin)
+        off = self.begin if self.gpos is None else 0
+        return self._glob(*kernels.flatip_topk(q, self.shard, k, id_offset=off))
 
 
-LAST_TOPK: dict = {}  # the latest sharded_topk_global call: path, rank, rescued queries
+LAST_TOPK: dict = {}  # the latest sharded_topk_global call: path, rank, rescued queries, host reads
+
+
+def _all_gather_rows(x: torch.Tensor, group, world: int) -> torch.Tensor:
+    out = torch.empty((world * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x.contiguous(), group=group)
+    return out
 
 
 def sharded_topk_global(queries: torch.Tensor, k: int, n_total: int, ops, merge: MergeFn, group=None,
-                        owner: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+                        owner: bool = True, shard_rows: Optional[Sequence[int]] = None
+                        ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Exact top-k over a row-sharded corpus with ONE corpus-wide threshold
     per query (rt_flatip_topk_shard_* of include/rtrec_hip.h).
 
+    0. whether every shard has the v4 plan and the corpus-wide (sampled,
+       total) stage counts are host arithmetic over the shard sizes
+       (``shard_rows``: every rank's row count, ``ops.plan`` =
+       rt_flatip_topk_shard_plan): no collective, no device read. Without
+       ``shard_rows`` the sizes are all-gathered first (one host read);
     1. every rank samples its shard (every stride-th 128-row stage: per query
-       the 32 largest group maxima, ``ops.sample``); one all-gather of the
-       [nq, 32] lists and one 24-byte all-reduce of the stage counts;
+       the union of each lane half's 16 largest group maxima, ``ops.sample``);
     2. the failure-safe rank for the corpus-wide sampled fraction
-       (``ops.rank``) and per query the rank-th largest of the union of all
+       (``ops.rank``), one all-gather of each list's top r entries (bf16,
+       rounded down) and per query the rank-th largest of the union of all
        ranks' lists (``ops.threshold``) — w.h.p. at most the query's k-th score
        over the WHOLE corpus;
     3. each rank keeps only its rows at or above it (``ops.search``): a query's
        candidates per shard shrink as the shards multiply, where a
        shard-local threshold keeps ~k per shard (:func:`sharded_topk_owner`);
-    4. the per-rank lists are merged as in :func:`sharded_topk_owner`
-       (``owner``: all-to-all, each rank its slice of the queries) or
-       :func:`sharded_topk` (all-gather, every rank all queries);
+    4. one ``all_to_all_single`` sends each query slice's lists to its owner,
+       which merges them (``merge``);
     5. a query whose merged list holds fewer than min(k, n_total) entries had a
-       threshold above its k-th: those queries (host-read flags, P < 1e-6
-       each) are searched again from -inf through :func:`sharded_topk`.
+       threshold above its k-th (P < 1e-6 each): the count of such queries is
+       summed over ranks on the device and read ONCE on the host — the only
+       host read of the call; when non-zero the flags are all-gathered and
+       those queries are searched again from -inf (:func:`sharded_topk`);
+    6. ``owner=True``: each rank returns its slice (``shard_range``) of the
+       queries (nq % world == 0). ``owner=False``: one all-gather of the merged
+       [nq/world, k] slices gives every rank every query's result (queries
+       padded to a multiple of world internally) — 2× the owner layout's
+       exchange, against world× for an all-gather of unmerged lists.
     Identical to one index over the whole corpus (scores depend only on the
     (query, row) pair). Shapes without the v4 plan on some rank take the
-    plain path (``ops.topk``) on every rank."""
+    plain path (``ops.topk``, all-to-all + owner merge) on every rank."""
     world, rank = _world(group)
     nq = queries.shape[0]
-    plain = sharded_topk_owner if owner else sharded_topk
     if world == 1:
         return ops.topk(queries, k)
     if owner and nq % world:
         raise ValueError(f"{nq} queries do not split over {world} ranks")
-    stride = kernels.shard_sample_stride(n_total)
-    smp = ops.sample(queries, k, stride)
+    n_pad = (-nq) % world
+    if n_pad:  # all-gather layout: copies of query 0 pad the last slice, dropped at the end
+        queries = torch.cat([queries, queries[:1].expand((n_pad,) + tuple(queries.shape[1:]))])
+    nqp = queries.shape[0]
+    per = nqp // world
     dev = queries.device
-    cnt = torch.tensor([1 if smp is not None else 0, smp[1][0] if smp else 0, smp[1][1] if smp else 0],
-                       dtype=torch.int64, device=dev)
-    dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-    supported, sampled, stages = (int(v) for v in cnt.tolist())
-    if supported != world:
+    reads = 0
+    if shard_rows is None:
+        mine = torch.tensor([ops.shard.shape[0]], dtype=torch.int64, device=dev)
+        shard_rows = [int(v) for v in _all_gather_rows(mine, group, world).tolist()]
+        reads += 1
+    if len(shard_rows) != world:
+        raise ValueError(f"shard_rows has {len(shard_rows)} entries for {world} ranks")
+    stride = kernels.shard_sample_stride(n_total)
+    plans = [ops.plan(nqp, int(rows), k, stride) for rows in shard_rows]
+
+    def finish(ms, mi):
+        if owner:
+            return ms, mi
+        fs, fi = _all_gather_rows(ms, group, world), _all_gather_rows(mi, group, world)
+        return fs[:nq], fi[:nq]
+
+    if any(p is None for p in plans):
         LAST_TOPK.clear()
-        LAST_TOPK.update({"path": "plain (no v4 plan on some shard)"})
-        return plain(queries, k, ops.topk, merge, group)
-    top = smp[0]
+        LAST_TOPK.update({"path": "plain (no v4 plan on some shard)", "host_reads": reads})
+        return finish(*sharded_topk_owner(queries, k, ops.topk, merge, group))
+    sampled = sum(p[0] for p in plans)
+    stages = sum(p[1] for p in plans)
+    top = ops.sample(queries, k, stride)[0]
     r = ops.rank(k, sampled, stages)  # the same on every rank (global counts)
     if r > 0:
         # the rank-th largest of the union needs only each list's top r; every
@@ -204,53 +253,42 @@ def sharded_topk_global(queries: torch.Tensor, k: int, n_total: int, ops, merge:
         # (the 16-bit patterns travel as a float16 view: a type both RCCL and
         # gloo move, and an all-gather copies bits without arithmetic)
         mine = _bf16_floor_bits(top[:, :r].contiguous()).view(torch.float16)
-        got = torch.empty((world * nq, r), dtype=torch.float16, device=dev)
-        dist.all_gather_into_tensor(got, mine, group=group)
-        lists = torch.full((world, nq, top.shape[1]), float("-inf"), dtype=torch.float32, device=dev)
-        lists[:, :, :r] = _bf16_bits_to_f32(got.view(torch.int16)).view(world, nq, r)
+        got = _all_gather_rows(mine, group, world)
+        lists = torch.full((world, nqp, top.shape[1]), float("-inf"), dtype=torch.float32, device=dev)
+        lists[:, :, :r] = _bf16_bits_to_f32(got.view(torch.int16)).view(world, nqp, r)
         thr = ops.threshold(lists, r)
     else:
-        thr = torch.full((nq,), -3.4028234663852886e38, dtype=torch.float32, device=dev)
+        thr = torch.full((nqp,), -3.4028234663852886e38, dtype=torch.float32, device=dev)
     s, i = ops.search(queries, k, thr)
-    if owner:
-        s = s.contiguous()
-        # ids cross as int32 when the corpus allows it (-1 padding survives)
-        i = i.to(torch.int32).contiguous() if n_total < 2 ** 31 else i.contiguous()
-        out_s, out_i = torch.empty_like(s), torch.empty_like(i)
-        dist.all_to_all_single(out_s, s, group=group)
-        dist.all_to_all_single(out_i, i, group=group)
-        out_i = out_i.to(torch.int64)
-        per = nq // world
-        ms, mi = merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
-    else:
-        all_s, all_i = all_gather_candidates(s, i, group)
-        ms, mi = merge(all_s, all_i, k)
+    s = s.contiguous()
+    # ids cross as int32 when the corpus allows it (-1 padding survives)
+    i = i.to(torch.int32).contiguous() if n_total < 2 ** 31 else i.contiguous()
+    out_s, out_i = torch.empty_like(s), torch.empty_like(i)
+    dist.all_to_all_single(out_s, s, group=group)
+    dist.all_to_all_single(out_i, i, group=group)
+    out_i = out_i.to(torch.int64)
+    ms, mi = merge(out_s.view(world, per, k), out_i.view(world, per, k), k)
     need = min(int(k), int(n_total))
-    bad = ((mi >= 0).sum(dim=1) < need).to(torch.uint8)
-    if owner:
-        allbad = torch.empty(world * bad.numel(), dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(allbad, bad.contiguous(), group=group)
-    else:
-        allbad = bad
-    idx = torch.nonzero(allbad).flatten()
-    n_bad = int(idx.numel())
+    bad = (mi >= 0).sum(dim=1) < need
+    if n_pad and rank == world - 1:  # padding queries never need a rescue
+        bad[per - n_pad:] = False
+    n_bad_dev = bad.sum().reshape(1).to(torch.int64)
+    dist.all_reduce(n_bad_dev, op=dist.ReduceOp.SUM, group=group)
+    n_bad = int(n_bad_dev.item())  # the one host read of the call
+    reads += 1
     if n_bad:
+        idx = torch.nonzero(_all_gather_rows(bad.to(torch.uint8), group, world)).flatten()
         fs, fi = sharded_topk(queries.index_select(0, idx), k, ops.topk, merge, group)
-        if owner:
-            per = nq // world
-            mine = (idx >= rank * per) & (idx < (rank + 1) * per)
-            rows = idx[mine] - rank * per
-            ms, mi = ms.clone(), mi.clone()
-            ms[rows] = fs[mine]
-            mi[rows] = fi[mine]
-        else:
-            ms, mi = ms.clone(), mi.clone()
-            ms[idx] = fs
-            mi[idx] = fi
+        sel = (idx >= rank * per) & (idx < (rank + 1) * per)
+        rows = idx[sel] - rank * per
+        ms, mi = ms.clone(), mi.clone()
+        ms[rows] = fs[sel]
+        mi[rows] = fi[sel]
     LAST_TOPK.clear()
     LAST_TOPK.update({"path": "global threshold", "stride": stride, "rank": r, "sampled_stages": sampled,
-                      "stages": stages, "rescued_queries": n_bad})
-    return ms, mi
+                      "stages": stages, "rescued_queries": n_bad, "host_reads": reads,
+                      "layout": "owner" if owner else "all-gather of merged slices"})
+    return finish(ms, mi)
 
 
 def _bf16_floor_bits(x: torch.Tensor) -> torch.Tensor:
@@ -674,10 +712,19 @@ class ShardedFlatIPIndex:
 
     def search_tensors(self, queries, k: int, excluded: Optional[Sequence[Sequence[int]]] = None
                        ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(scores, global positions) [nq, k] on every rank. Without exclusions
+        the search is :func:`sharded_topk_global` (corpus-wide threshold, owner
+        merge, all-gather of the merged slices; the plain owner merge where the
+        shape has no v4 plan); per-query exclusions take :func:`sharded_topk`
+        with a bitmap per shard."""
         if self.shard is None:
             raise ValueError("Index not built yet")
         q = self._prep(queries)
-        return sharded_topk(q, k, self._local(excluded), kernels.topk_merge, self.group)
+        if excluded is not None:
+            return sharded_topk(q, k, self._local(excluded), kernels.topk_merge, self.group)
+        sizes = [shard_range(self.n_total, self.world, r)[1] for r in range(self.world)]
+        return sharded_topk_global(q, k, self.n_total, ShardOps(self.shard, self.begin), kernels.topk_merge,
+                                   self.group, owner=False, shard_rows=sizes)
 
     def search(self, queries, k: int = 10) -> Tuple[np.ndarray, np.ndarray]:
         s, i = self.search_tensors(queries, k)

@@ -181,11 +181,25 @@ def shard_sample_stride(n_total: int, nt: int = 128, max_stride: int = 64) -> in
     return int(max(1, min(max_stride, stages // 32)))
 
 
+def flatip_topk_shard_plan(nq: int, n_rows: int, d: int, dtype: torch.dtype, k: int, stride: int):
+    """Host-only plan of a shard of ``n_rows`` rows (rt_flatip_topk_shard_plan):
+    the (sampled, total) 128-row stage counts rt_flatip_topk_shard_sample would
+    report, or None when the shape has no v4 plan. No device work, no sync."""
+    counts = (ctypes.c_int64 * 2)()
+    rc = native.lib().rt_flatip_topk_shard_plan(int(nq), int(n_rows), int(d), native.dtype_code(dtype), int(k),
+                                                int(stride), ctypes.cast(counts, ctypes.c_void_p))
+    if rc != 0:
+        return None
+    return int(counts[0]), int(counts[1])
+
+
 def flatip_topk_shard_sample(queries: torch.Tensor, items: torch.Tensor, k: int, stride: int):
-    """This shard's sample (rt_flatip_topk_shard_sample): per query the 32
-    largest sampled group maxima [nq, 32] f32 (descending) and the (sampled,
-    total) 128-row stage counts of the shard. None when the shape has no v4
-    plan (f16/bf16, d <= 128, k <= 128, >= 65,536 rows or forced)."""
+    """This shard's sample (rt_flatip_topk_shard_sample): per query the union
+    of each lane half's 16 largest sampled group maxima [nq, 32] f32
+    (descending; a subset of the 32 largest, so thresholds drawn from it are
+    at or below the exact ones) and the (sampled, total) 128-row stage counts
+    of the shard. None when the shape has no v4 plan (f16/bf16, d <= 128,
+    k <= 128, >= 65,536 rows or forced)."""
     native.require_device(queries, items, what="flatip_topk_shard_sample")
     queries, items = queries.contiguous(), items.contiguous()
     nq, d = queries.shape

@@ -85,6 +85,7 @@ SIGNATURES = {
     "rt_topk_merge": (c_int, [vp, vp, c_i64, c_int, c_int, c_int, vp, vp, vp]),
     "rt_flatip_topk_tuning": (c_int, [c_int, c_int, c_int]),
     "rt_flatip_topk_shard_workspace_bytes": (c_size, [c_i64, c_i64, c_int, c_int, c_int]),
+    "rt_flatip_topk_shard_plan": (c_int, [c_i64, c_i64, c_int, c_int, c_int, c_int, vp]),
     "rt_flatip_topk_shard_sample": (c_int, [vp, c_i64, vp, c_i64, c_int, c_int, c_int, c_int, vp, vp, vp, c_size,
                                             vp]),
     "rt_topk_sample_rank": (c_int, [c_int, c_i64, c_i64, vp]),

@@ -203,7 +203,8 @@ def _gather_worker(rank, world, n, d, seed, counts, skew):
 @pytest.mark.parametrize("world,counts,skew", [(2, [13, 29], False), (4, [7, 0, 31, 16], False),
                                                (2, [40, 9], True), (3, [5, 5, 5], True),
                                                (4, [512] * 4, False), (4, [512] * 4, True),
-                                               (3, [300, 0, 417], False)])
+                                               (3, [300, 0, 417], False), (8, [1024] * 8, False),
+                                               (8, [1024] * 8, True), (8, [100, 0, 57, 300, 1, 2, 3, 64], False)])
 def test_sharded_gather_rows_gloo(world, counts, skew):
     """C5 exchange: ragged per-rank batches (one empty), ids skewed onto one
     owner (the other windows own nothing; at 4 x 512 positions that overflows
@@ -255,7 +256,8 @@ def _scatter_worker(rank, world, n, d, b, seed, skew=False):
                                  scatter_add=scatter_add, check=True)
 
 
-@pytest.mark.parametrize("world,b,skew", [(2, 64, False), (3, 64, False), (4, 2048, False), (4, 2048, True)])
+@pytest.mark.parametrize("world,b,skew", [(2, 64, False), (3, 64, False), (4, 2048, False), (4, 2048, True),
+                                          (8, 2048, False), (8, 2048, True)])
 def test_sharded_scatter_add_rows_gloo(world, b, skew):
     """Trainable C5 table: row gradients of the global batch summed over ranks
     and added by their owners into their shards — by one reduce-scatter of
@@ -324,11 +326,67 @@ def _c5_worker(rank, world, n, d, b, seed):
     np.testing.assert_allclose(grad_shard.numpy(), ref_g[beg:beg + cnt], rtol=1e-5, atol=1e-7)
 
 
-def test_sharded_inbatch_step_gloo():
-    _run(2, _c5_worker, 401, 16, 24, 5)
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_inbatch_step_gloo(world):
+    _run(world, _c5_worker, 401, 16, 24, 5)
 
 
-def _global_thr_worker(rank, world, n, d, nq, k, seed, owner, force_rescue):
+class CpuShardOps:
+    """CPU restatements of the six per-rank calls of sharded_topk_global
+    (tests may use the oracle): scores are the oracle's fmaf chains
+    (flat_ip_search over the whole shard), ids are global positions
+    (``begin + row`` or ``gpos[row]``), the plan always applies to a
+    non-empty shard, ``force_rescue`` picks an unsafe rank of 1."""
+
+    def __init__(self, shard, begin=0, gpos=None, force_rescue=False):
+        self.shard = shard
+        self.begin, self.gpos, self.force = int(begin), gpos, force_rescue
+
+    def _glob(self, i):
+        if self.gpos is None:
+            return np.where(i >= 0, i + self.begin, -1)
+        return np.where(i >= 0, self.gpos[np.maximum(i, 0)], -1)
+
+    def plan(self, nq, rows, kk, stride):
+        if rows <= 0:
+            return None
+        stages = -(-rows // 128)
+        return len(range(0, stages, stride)), stages
+
+    def sample(self, q, kk, stride):
+        top, cnt = orc.shard_sample(q.numpy(), self.shard.numpy(), stride)
+        return torch.from_numpy(top), cnt
+
+    def rank(self, kk, sampled, stages):
+        return 1 if self.force else orc.sample_rank(kk, sampled, stages)
+
+    def threshold(self, lists, r):
+        u = -np.sort(-lists.numpy().transpose(1, 0, 2).reshape(lists.shape[1], -1), axis=1)
+        t = u[:, r - 1]
+        return torch.from_numpy(np.where(np.isfinite(t), t, -np.finfo(np.float32).max).astype(np.float32))
+
+    def search(self, q, kk, thr):
+        n = self.shard.shape[0]
+        s, i = orc.flat_ip_search(q.numpy(), self.shard.numpy(), n)  # every row, (score desc, id asc)
+        out_s = np.full((q.shape[0], kk), -np.finfo(np.float32).max, np.float32)
+        out_i = np.full((q.shape[0], kk), -1, np.int64)
+        for r in range(q.shape[0]):
+            m = min(kk, int(np.sum(s[r] >= thr[r].item())))
+            out_s[r, :m] = s[r, :m]
+            out_i[r, :m] = self._glob(i[r, :m])
+        return torch.from_numpy(out_s), torch.from_numpy(out_i)
+
+    def topk(self, q, kk):
+        s, i = orc.flat_ip_search(q.numpy(), self.shard.numpy(), kk)
+        return torch.from_numpy(s), torch.from_numpy(self._glob(i))
+
+
+def _cpu_merge(s, i, kk):
+    ms, mi = orc.topk_merge(s.numpy(), i.numpy(), kk)
+    return torch.from_numpy(ms), torch.from_numpy(mi)
+
+
+def _global_thr_worker(rank, world, n, d, nq, k, seed, owner, force_rescue, pass_rows=True):
     from rtrec_amd.dist.sharded import LAST_TOPK, sharded_topk_global
     from rtrec_amd import kernels as K
     rng = np.random.default_rng(seed)
@@ -336,41 +394,10 @@ def _global_thr_worker(rank, world, n, d, nq, k, seed, owner, force_rescue):
     corpus[n - 1] = corpus[0]  # a tie across the shard boundary
     queries = _dyadic(rng, nq, d)
     b, c = shard_range(n, world, rank)
-    shard = corpus[b:b + c]
-
-    class Ops:  # CPU restatements of the five per-rank calls (tests may use the oracle)
-        def sample(self, q, kk, stride):
-            top, cnt = orc.shard_sample(q.numpy(), shard, stride)
-            return torch.from_numpy(top), cnt
-
-        def rank(self, kk, sampled, stages):
-            return 1 if force_rescue else orc.sample_rank(kk, sampled, stages)
-
-        def threshold(self, lists, r):
-            u = -np.sort(-lists.numpy().transpose(1, 0, 2).reshape(lists.shape[1], -1), axis=1)
-            t = u[:, r - 1]
-            return torch.from_numpy(np.where(np.isfinite(t), t, -np.finfo(np.float32).max).astype(np.float32))
-
-        def search(self, q, kk, thr):
-            sc = (q.numpy().astype(np.float64) @ shard.astype(np.float64).T).astype(np.float32)
-            out_s = np.full((q.shape[0], kk), -np.finfo(np.float32).max, np.float32)
-            out_i = np.full((q.shape[0], kk), -1, np.int64)
-            for r in range(q.shape[0]):
-                keep = np.nonzero(sc[r] >= thr[r].item())[0]
-                order = keep[np.lexsort((keep, -sc[r][keep]))][:kk]
-                out_s[r, :order.size] = sc[r][order]
-                out_i[r, :order.size] = order + b
-            return torch.from_numpy(out_s), torch.from_numpy(out_i)
-
-        def topk(self, q, kk):
-            s, i = orc.flat_ip_search(q.numpy(), shard, kk, id_offset=b)
-            return torch.from_numpy(s), torch.from_numpy(i)
-
-    def merge(s, i, kk):
-        ms, mi = orc.topk_merge(s.numpy(), i.numpy(), kk)
-        return torch.from_numpy(ms), torch.from_numpy(mi)
-
-    got_s, got_i = sharded_topk_global(torch.from_numpy(queries), k, n, Ops(), merge, owner=owner)
+    ops = CpuShardOps(torch.from_numpy(corpus[b:b + c]), b, force_rescue=force_rescue)
+    rows = [shard_range(n, world, r)[1] for r in range(world)] if pass_rows else None
+    got_s, got_i = sharded_topk_global(torch.from_numpy(queries), k, n, ops, _cpu_merge, owner=owner,
+                                       shard_rows=rows)
     if owner:
         qb, qc = shard_range(nq, world, rank)
         ref_s, ref_i = orc.flat_ip_search(queries[qb:qb + qc], corpus, k)
@@ -380,19 +407,25 @@ def _global_thr_worker(rank, world, n, d, nq, k, seed, owner, force_rescue):
     np.testing.assert_array_equal(got_s.numpy(), ref_s)
     assert LAST_TOPK["path"] == "global threshold"
     assert LAST_TOPK["stride"] == K.shard_sample_stride(n)
+    # host reads: the rescue count only (plus the shard-size all-gather without shard_rows)
+    assert LAST_TOPK["host_reads"] == (1 if pass_rows else 2)
     if force_rescue:
         assert LAST_TOPK["rescued_queries"] > 0
 
 
-@pytest.mark.parametrize("world,n,k,owner,force", [(2, 16384, 10, True, False), (3, 16384, 100, False, False),
-                                                   (4, 9000, 50, True, False), (2, 16384, 100, True, True)])
-def test_sharded_topk_global_threshold_gloo(world, n, k, owner, force):
+@pytest.mark.parametrize("world,n,nq,k,owner,force,rows", [
+    (2, 16384, 24, 10, True, False, True), (3, 16384, 24, 100, False, False, True),
+    (4, 9000, 24, 50, True, False, False), (2, 16384, 24, 100, True, True, True),
+    (8, 20000, 24, 100, True, False, True), (8, 20000, 21, 100, False, False, True),
+    (8, 20000, 24, 100, True, True, True), (8, 20000, 13, 10, False, True, False)])
+def test_sharded_topk_global_threshold_gloo(world, n, nq, k, owner, force, rows):
     """C4 at N GPUs with ONE corpus-wide threshold per query (ranks' shard
     samples all-gathered, the failure-safe rank of the corpus-wide sampled
     fraction): exact against one index over the whole corpus, owner and
-    all-gather layouts; forcing an unsafe rank (threshold above the k-th)
+    all-gather layouts (queries padded to a multiple of the world), up to the
+    machine's 8 ranks; forcing an unsafe rank (threshold above the k-th)
     exercises the rescue of the short queries from -inf."""
-    _run(world, _global_thr_worker, n, 32, 24, k, 13, owner, force)
+    _run(world, _global_thr_worker, n, 32, nq, k, 13, owner, force, rows)
 
 
 def test_sample_rank_matches_library():
@@ -421,3 +454,174 @@ def test_bf16_floor_bits_round_down():
     assert float(gap.max()) <= 2.0 ** -7  # one bf16 ulp at most
     z = torch.randn(1000, generator=g).to(torch.bfloat16).float()
     assert torch.equal(_bf16_bits_to_f32(_bf16_floor_bits(z)), z)
+
+
+# ---------------------------------------------------------------------------
+# HipShardedFlatIPIndex behind the reference plugin API (RetrievalEngine
+# index_type "hip_flat_sharded"), per-rank compute on the CPU oracle
+def _cpu_index_cls(force_rescue=False):
+    from rtrec_amd.serving.retrieval import HipShardedFlatIPIndex
+
+    class CpuShardedIndex(HipShardedFlatIPIndex):
+        """The product class with its three device hooks on the CPU oracle:
+        storage on the CPU, oracle renorm (Faiss rule), oracle ops/merge. The
+        id maps, layout, add, filter, tiling, save/load and every collective
+        are the product code."""
+
+        def _dev(self):
+            return torch.device("cpu")
+
+        def _renorm_(self, t):
+            a = t.numpy()
+            orc.normalize_L2(a)
+            return t
+
+        def _ops(self, rows):
+            gpos = self.gpos.numpy() if self.gpos is not None else None
+            return CpuShardOps(rows.float(), self.begin, gpos, force_rescue=force_rescue)
+
+        def _merge(self, s, i, k):
+            return _cpu_merge(s, i, k)
+    return CpuShardedIndex
+
+
+def _ref_lists(corpus, queries, k, metric, ids, filter_ids=None):
+    """One whole-corpus index (the HipFlatIPIndex / FaissIndex contract) on the oracle."""
+    from rtrec_amd.serving.retrieval import _lists_from_positions
+    x, q = corpus.copy(), queries.copy()
+    if metric == "cosine":
+        orc.normalize_L2(x)
+        orc.normalize_L2(q)
+    ks = min(2 * k, len(x)) if filter_ids else k
+    s, i = orc.flat_ip_search(q, x, ks)
+    return _lists_from_positions(s, i, {p: v for p, v in enumerate(ids)}, k, filter_ids)
+
+
+def _index_worker(rank, world, n, d, nq, k, metric, tile, tmp, force_rescue):
+    from rtrec_amd.dist import sharded as sh
+    from rtrec_amd.serving.retrieval import RetrievalEngine, register_index
+    register_index("hip_flat_sharded", _cpu_index_cls(force_rescue))
+    rng = np.random.default_rng(21)
+    corpus = _dyadic(rng, n, d) if metric == "inner_product" else rng.standard_normal((n, d)).astype(np.float32)
+    corpus[n - 1] = corpus[3]          # an exact tie across shards: the lower position wins
+    queries = _dyadic(rng, nq, d) if metric == "inner_product" else rng.standard_normal((nq, d)).astype(np.float32)
+    ids = [f"item_{p}" for p in range(n)]
+    cfg = {"index_type": "hip_flat_sharded", "embedding_dim": d, "top_k": k,
+           "hip_flat_sharded": {"metric": metric, "query_tile": tile}}
+    eng = RetrievalEngine(cfg)
+    assert eng.index.world == world and eng.index.rank == rank
+    eng.build_index(corpus, ids)
+    got_i, got_s, met = eng.retrieve(queries, k)
+    ref_i, ref_s = _ref_lists(corpus, queries, k, metric, ids)
+    assert got_i == ref_i and got_s == ref_s
+    assert met["num_results"] == nq * min(k, n)
+    assert sh.LAST_TOPK["path"] == "global threshold"
+    if force_rescue:
+        assert sh.LAST_TOPK["rescued_queries"] > 0
+    # a 1-D query is reshaped; the md5 cache answers the repeat
+    one_i, _, _ = eng.retrieve(queries[0], k)
+    assert one_i == [ref_i[0]]
+    _, _, m2 = eng.retrieve(queries[0], k)
+    assert m2["cache_hit"]
+    # filter_ids: k_search = min(2k, N) over-fetch, then the filter
+    allow = [ids[p] for p in range(0, n, 3)]
+    f_i, f_s, _ = eng.retrieve(queries, k, allow)
+    r_i, r_s = _ref_lists(corpus, queries, k, metric, ids, allow)
+    assert f_i == r_i and f_s == r_s
+    # owner layout: this rank's slice of each query tile
+    nq_own = nq - nq % world
+    s_own, p_own = eng.index.search_tensors(queries[:nq_own], k, layout="owner")
+    s_all, p_all = eng.index.search_tensors(queries[:nq_own], k)
+    tile_eff = max(tile - tile % world, world)  # the index's tiles hold a multiple of the world
+    rows = []
+    for t0 in range(0, nq_own, tile_eff):
+        qb, qc = shard_range(min(tile_eff, nq_own - t0), world, rank)
+        rows.extend(range(t0 + qb, t0 + qb + qc))
+    np.testing.assert_array_equal(p_own.numpy(), p_all.numpy()[rows])
+    np.testing.assert_array_equal(s_own.numpy(), s_all.numpy()[rows])
+    # incremental add (Kafka item_update path): new global rows spread over the ranks
+    extra = _dyadic(rng, 37, d) if metric == "inner_product" else rng.standard_normal((37, d)).astype(np.float32)
+    extra[5] = corpus[3]               # ties the earlier row: the older (lower) position wins
+    new_ids = [f"new_{j}" for j in range(37)]
+    eng.update_index(extra, new_ids)
+    assert eng.get_metrics()["index_size"] == n + 37
+    assert sum(eng.index.shard_sizes) == n + 37
+    assert max(eng.index.shard_sizes) - min(eng.index.shard_sizes) <= 2
+    all_x, all_ids = np.concatenate([corpus, extra]), ids + new_ids
+    a_i, a_s, _ = eng.retrieve(queries, k)
+    r_i, r_s = _ref_lists(all_x, queries, k, metric, all_ids)
+    assert a_i == r_i and a_s == r_s
+    # per-shard save, same-world load
+    path = os.path.join(tmp, "idx")
+    eng.save(path)
+    eng2 = RetrievalEngine(cfg)
+    eng2.load(path)
+    b_i, b_s, _ = eng2.retrieve(queries, k)
+    assert b_i == r_i and b_s == r_s
+    assert eng2.index.current_size == n + 37
+    # errors of the FaissIndex contract
+    fresh = RetrievalEngine(cfg).index
+    with pytest.raises(ValueError, match="Index not built yet"):
+        fresh.search(queries, k)
+    with pytest.raises(ValueError, match="No index to save"):
+        fresh.save(path + "_none")
+
+
+@pytest.mark.parametrize("world,n,nq,k,metric,tile,force", [
+    (2, 3001, 19, 10, "cosine", 65536, False), (4, 2500, 23, 50, "inner_product", 8, False),
+    (8, 4099, 29, 100, "inner_product", 65536, False), (8, 3000, 17, 20, "cosine", 8, True)])
+def test_sharded_index_through_retrieval_engine_gloo(tmp_path, world, n, nq, k, metric, tile, force):
+    """the multi-GPU index behind the reference plugin API —
+    RetrievalEngine({"index_type": "hip_flat_sharded"}) at world 2/4/8 equals
+    one whole-corpus index id for id (string ids, scores, exact ties, 1-D
+    queries, the cache, filter_ids over-fetch, add, per-shard save/load,
+    query tiles, owner layout, forced rescues)."""
+    _run(world, _index_worker, n, 32, nq, k, metric, tile, str(tmp_path), force)
+
+
+def _reshard_save_worker(rank, world, n, d, tmp):
+    from rtrec_amd.serving.retrieval import RetrievalEngine, register_index
+    register_index("hip_flat_sharded", _cpu_index_cls())
+    rng = np.random.default_rng(8)
+    corpus = _dyadic(rng, n, d)
+    eng = RetrievalEngine({"index_type": "hip_flat_sharded", "embedding_dim": d,
+                           "hip_flat_sharded": {"metric": "inner_product"}})
+    eng.build_index(corpus, [f"i{p}" for p in range(n)])
+    eng.update_index(_dyadic(rng, 11, d), [f"n{j}" for j in range(11)])
+    eng.save(os.path.join(tmp, "w"))
+
+
+def _reshard_load_worker(rank, world, n, d, tmp):
+    from rtrec_amd.serving.retrieval import RetrievalEngine, register_index
+    register_index("hip_flat_sharded", _cpu_index_cls())
+    rng = np.random.default_rng(8)
+    corpus = np.concatenate([_dyadic(rng, n, d), _dyadic(rng, 11, d)])
+    ids = [f"i{p}" for p in range(n)] + [f"n{j}" for j in range(11)]
+    q = _dyadic(np.random.default_rng(9), 9, d)
+    cfg = {"index_type": "hip_flat_sharded", "embedding_dim": d, "hip_flat_sharded": {"metric": "inner_product"}}
+    eng = RetrievalEngine(cfg)
+    eng.load(os.path.join(tmp, "w"))        # saved by 2 ranks, loaded by `world`: re-sharded
+    got = eng.retrieve(q, 15)[:2]
+    assert got == _ref_lists(corpus, q, 15, "inner_product", ids)
+    assert eng.index.shard_sizes == [shard_range(n + 11, world, r)[1] for r in range(world)]
+    eng2 = RetrievalEngine(cfg)
+    eng2.load(os.path.join(tmp, "single"))  # a single-GPU HipFlatIPIndex save
+    assert eng2.retrieve(q, 15)[:2] == got
+
+
+def test_sharded_index_reshards_on_load_gloo(tmp_path):
+    """A per-shard save from 2 ranks loads on 4 (rows re-sharded by global
+    position), and a single-GPU index save (one .faiss + .pkl) loads sharded."""
+    import pickle
+
+    from rtrec_amd.serving.retrieval import write_flat_index
+    n, d = 203, 16
+    _run(2, _reshard_save_worker, n, d, str(tmp_path))
+    rng = np.random.default_rng(8)
+    corpus = np.concatenate([_dyadic(rng, n, d), _dyadic(rng, 11, d)])
+    ids = [f"i{p}" for p in range(n)] + [f"n{j}" for j in range(11)]
+    write_flat_index(tmp_path / "single.faiss", corpus, True)
+    with open(tmp_path / "single.pkl", "wb") as f:
+        pickle.dump({"id_map": dict(enumerate(ids)), "reverse_id_map": {v: p for p, v in enumerate(ids)},
+                     "current_size": len(ids), "config": {"metric": "inner_product"}}, f)
+    _run(4, _reshard_load_worker, n, d, str(tmp_path))

@@ -131,3 +131,69 @@ def test_c5_sharded_step_captures_in_a_graph(device):
             assert torch.equal(a, c)
     torch.cuda.synchronize()
     assert int(status[0]) == int(status[1]) and int(status[0]) > 0
+
+
+def test_sharded_index_engine_single_rank_matches_flat_index(device, tmp_path):
+    """RetrievalEngine({"index_type": "hip_flat_sharded"}) on one rank equals
+    HipFlatIPIndex id for id (cosine fp32 and inner-product f16), through add,
+    filter_ids and a per-shard save/load."""
+    from rtrec_amd.serving.retrieval import HipFlatIPIndex, RetrievalEngine
+    rng = np.random.default_rng(23)
+    for metric, st, n in (("cosine", "float32", 5000), ("inner_product", "float16", 70_000)):
+        corpus = (rng.integers(-8, 9, size=(n, 64)) / 64.0).astype(np.float32)
+        corpus[-1] = corpus[2]
+        q = (rng.integers(-8, 9, size=(50, 64)) / 64.0).astype(np.float32)
+        ids = [f"i{p}" for p in range(n)]
+        cfg = {"index_type": "hip_flat_sharded", "embedding_dim": 64,
+               "hip_flat_sharded": {"metric": metric, "storage_dtype": st, "device": str(device)}}
+        eng = RetrievalEngine(cfg)
+        eng.build_index(corpus, ids)
+        flat = HipFlatIPIndex({"dimension": 64, "metric": metric, "storage_dtype": st, "device": str(device)})
+        flat.build(corpus, ids)
+        assert eng.retrieve(q, 100)[:2] == flat.search(q, 100)
+        assert eng.retrieve(q, 7, ids[::3])[:2] == flat.search(q, 7, ids[::3])
+        extra = (rng.integers(-8, 9, size=(99, 64)) / 64.0).astype(np.float32)
+        eng.update_index(extra, [f"x{j}" for j in range(99)])
+        flat.add(extra, [f"x{j}" for j in range(99)])
+        assert eng.retrieve(q, 100)[:2] == flat.search(q, 100)
+        eng.save(str(tmp_path / metric))
+        eng2 = RetrievalEngine(cfg)
+        eng2.load(str(tmp_path / metric))
+        assert eng2.retrieve(q, 100)[:2] == flat.search(q, 100)
+
+
+def test_sharded_index_two_ranks_on_one_gpu(tmp_path):
+    """HipShardedFlatIPIndex with two ranks (gloo, both on cuda:0; RCCL wants
+    one GPU per rank): the corpus-wide-threshold search with its real HIP
+    kernels and exchange steps equals one whole-corpus HipFlatIPIndex id for id
+    (tools/sharded_index_ranks.py: k 100 and 10, filter_ids, add, owner slice,
+    forced rescue). Started as child processes (torch.distributed.run)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "ranks.json")
+    env = dict(os.environ)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(repo, "real-time-recommendation-system-with-feature-store_amd"),
+                                         repo, env.get("PYTHONPATH", "")])
+    proc = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                           "--master-addr", "127.0.0.1", "--master-port", str(port),
+                           os.path.join(repo, "tools", "sharded_index_ranks.py"), out],
+                          cwd=repo, env=env, capture_output=True, text=True, timeout=240)
+    reports = []
+    for r in range(2):
+        p = f"{out}.rank{r}"
+        if os.path.exists(p):
+            with open(p) as f:
+                reports.append(json.load(f))
+    assert proc.returncode == 0, (proc.stdout[-3000:], proc.stderr[-3000:], reports)
+    assert len(reports) == 2 and all(r["ok"] for r in reports), reports
+    paths = [c["path"].get("path") for c in reports[0]["checks"] if "path" in c]
+    assert "global threshold" in paths and any(p and p.startswith("plain") for p in paths), paths
+    rescue = [c for c in reports[0]["checks"] if c["name"] == "forced rescue"][0]
+    assert rescue["path"]["rescued_queries"] > 0
