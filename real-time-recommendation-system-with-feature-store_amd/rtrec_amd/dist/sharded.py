@@ -523,7 +523,7 @@ def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_id
                              grad_rows: torch.Tensor, group=None,
                              scatter_add: Optional[Callable] = None,
                              status: Optional[torch.Tensor] = None, check: bool = False,
-                             exchange: str = "auto") -> torch.Tensor:
+                             exchange: str = "auto", overflow: Optional[bool] = None) -> torch.Tensor:
     """Backward of :func:`sharded_gather_rows` for a TRAINABLE row-sharded table
     (the nn.Embedding path a2 under C5 sharding, SURVEY §8(e) "next"): every rank
     holds its own contribution to d loss / d rows for the whole global batch
@@ -539,8 +539,10 @@ def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_id
       order within an owner) and ONE reduce-scatter leaves each owner the sum
       over ranks of its own segment, which it scatter-adds into its shard:
       (N-1)·cap·D·4 bytes per rank, about half of the all-reduce below. The
-      overflow flag (a skewed batch) is read on the host; an overflow re-runs
-      as ``"allreduce"``.
+      overflow flag (a skewed batch) is read on the host — unless the caller
+      already knows it (``overflow``: e.g. the gather of the same ids in
+      :func:`sharded_inbatch_step` decided it, so no second host read); an
+      overflow re-runs as ``"allreduce"``.
     * ``"allreduce"`` (sync-free): one all-reduce (sum, fp32) of the whole
       [B_total, D] gradient, then every rank scatter-adds the rows of its own
       window (``rt_scatter_add_rows_f32`` skips ids outside [0, rows)).
@@ -571,7 +573,9 @@ def sharded_scatter_add_rows(grad_shard: torch.Tensor, row_begin: int, global_id
         exchange = "allreduce" if _capturing(g) else "segments"
     if exchange == "segments":
         cap = segment_capacity(n_pos, world)
-        if cap >= n_pos or not bool((own.counts > cap).any()):
+        if overflow is None:
+            overflow = cap < n_pos and bool((own.counts > cap).any())  # host read
+        if not overflow:
             dst = torch.where(own.valid & (own.slot < cap), own.own.to(torch.int64) * cap + own.slot,
                               torch.full_like(own.slot, world * cap))
             send = torch.zeros((world * cap + 1, d), dtype=torch.float32, device=dev)
@@ -607,7 +611,10 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     rank·b + i) with ``rt_inbatch_loss_fwd_bwd``; the loss is averaged over
     ranks by one 8-byte all-reduce. The step runs three collectives: the
     ids + windows all-gather, the segment all-gather (``exchange``, see
-    :func:`sharded_gather_rows`), the loss all-reduce.
+    :func:`sharded_gather_rows`), the loss all-reduce (plus, for a trainable
+    table, the windows all-gather and the owner reduce-scatter of the row
+    gradients, which reuse the gather's overflow decision: no second host
+    read).
 
     The item table is a frozen feature table in the reference
     (src/training/datasets/movielens.py:61-63,116), so by default the item-row
@@ -615,8 +622,9 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     contribution [B_total, D]. With ``grad_shard`` (a trainable table) they are
     summed and added into the owners' shards (:func:`sharded_scatter_add_rows`).
     At N = 1 the same code runs with its collectives skipped. The segment
-    exchange reads one overflow flag on the host; under hipGraph capture (or
-    ``exchange="max"``) the step is sync-free. Returns (global mean loss [1],
+    exchange reads one overflow flag on the host (once per step, trainable
+    table included); under hipGraph capture (or ``exchange="max"``) the step
+    is sync-free. Returns (global mean loss [1],
     d loss/d user_emb, d loss/d rows (this rank's part))."""
     world, rank = _world(group)
     b = user_emb.shape[0]
@@ -634,8 +642,12 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     if status is not None:
         _status_update(status, False, n_valid, owned)
     if grad_shard is not None:
+        # the gather of these same ids already settled whether a segment overflows
+        # (same positions, same segment_capacity): reuse it instead of a second host read
+        mode = rec.get("mode")
+        sx = "segments" if mode == "owner segments" else "allreduce" if world > 1 else exchange
         sharded_scatter_add_rows(grad_shard, row_begin, gids, dp.float() / world, group, scatter_add,
-                                 exchange=("allreduce" if exchange == "max" else exchange))
+                                 exchange=sx, overflow=False if sx == "segments" else None)
     # each rank's loss is a mean over its own b users; the global mean averages them
     return lv / world, du / world, dp / world
 

@@ -243,9 +243,9 @@ def _zero_on_entry(layer, zero_buf: Optional[torch.Tensor]):
 def chain_forward(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
                   normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
                   stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0,
-                  zero_buf: Optional[torch.Tensor] = None) -> ChainCtx:
+                  zero_buf: Optional[torch.Tensor] = None, seed_base: Optional[int] = None) -> ChainCtx:
     """Run the block chain (see ``_forward_plan`` for the arguments)."""
-    ctx, layers = _forward_plan(blocks, src, ids, normalize, seed_offset, stats_arena, seg_split)
+    ctx, layers = _forward_plan(blocks, src, ids, normalize, seed_offset, stats_arena, seg_split, seed_base)
     _zero_on_entry(layers[0], zero_buf)
     st = _stream(src)
     for a in layers:
@@ -282,14 +282,28 @@ def _launch_fwd(group: list, st) -> None:
             call("rt_linear_fwd_f32_multi", arr, len(group), st)
 
 
+def layer_seed(seed_base: int, layer: int) -> int:
+    """Dropout seed of one layer of a chain with a fixed ``seed_base``
+    (splitmix64 of the pair): the kernel adds the device step counter
+    (``seed_offset``), so the masks change every step while an eager step and
+    a graph replay of the same step draw the same masks."""
+    z = (seed_base * 0x100000001B3 + (layer + 1) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
 def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Tensor] = None,
                   normalize: bool = True, seed_offset: Optional[torch.Tensor] = None,
-                  stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0):
+                  stats_arena: Optional[torch.Tensor] = None, seg_split: int = 0,
+                  seed_base: Optional[int] = None):
     """Allocate the chain's activations and build its per-layer launch
     arguments (launched by the callers above). ``src`` is the dense input [rows, k0] (fp32) or a
     feature table when ``ids`` selects its rows (fused gather). ``seg_split`` > 0
     runs two tower calls in one chain: rows [0, seg_split) and [seg_split, m)
-    are separate BatchNorm batches (running stats updated in that order)."""
+    are separate BatchNorm batches (running stats updated in that order).
+    ``seed_base``: fixed per-layer dropout seeds (``layer_seed``) instead of a
+    fresh host seed per call."""
     native.require_device(src, what="tower forward")
     if src.dtype != torch.float32:
         raise TypeError("tower input must be fp32 (the reference towers are fp32)")
@@ -394,7 +408,8 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
             ctx.zs.append(z)
             ctx.save_mean.append(None)
             ctx.save_invstd.append(None)
-            ctx.seeds.append(next(_seed_counter) * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
+            ctx.seeds.append(layer_seed(seed_base, li) if seed_base is not None else
+                             next(_seed_counter) * 0x9E3779B97F4A7C15 & 0xFFFFFFFFFFFFFFFF)
             ctx.drop_ps.append(b.drop_p())
             ctx.bn_modes.append(b.bn_mode())
             cur_src, cur_ids, ld = z, None, lin.out_features

@@ -14,6 +14,7 @@ hipGraph and replayed (``capture``/``replay``).
 from __future__ import annotations
 
 import ctypes
+import itertools
 from typing import Dict, Optional
 
 import torch
@@ -24,6 +25,9 @@ from ..models.fused import (blocks_from_sequential, chain_backward, chain_backwa
 from ..models.two_tower import TwoTowerModel
 from ..native import call, ptr
 from ..profiling import TIMER
+
+
+_STEP_SEEDS = itertools.count(0x5EED)
 
 
 def _adjacent_or_cat(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -39,7 +43,7 @@ def _adjacent_or_cat(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
 class FusedTrainStep:
     def __init__(self, model: TwoTowerModel, lr: float = 1e-3, weight_decay: float = 1e-5, max_norm: float = 1.0,
                  betas=(0.9, 0.999), eps: float = 1e-8, explicit_weight: float = 0.7,
-                 in_batch_weight: float = 0.3, process_group=None):
+                 in_batch_weight: float = 0.3, process_group=None, dropout_seed: Optional[int] = None):
         self.model = model
         self.pg = process_group
         self.slab = model.slab()
@@ -51,6 +55,17 @@ class FusedTrainStep:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self.lr_dev = torch.tensor([lr], dtype=torch.float32, device=dev)
         self.seed_dev = torch.zeros(1, dtype=torch.int64, device=dev)   # dropout mask counter
+        # fixed per-chain dropout seed bases (+ the device counter above, bumped by
+        # every step's clip+Adam): an eager step and a replay of the captured
+        # step at the same counter draw identical masks
+        if dropout_seed is None:  # deterministic per process, distinct per step object
+            dropout_seed = next(_STEP_SEEDS)
+        self.dropout_seed = int(dropout_seed)
+        self._sb_user, self._sb_pos, self._sb_neg = (self.dropout_seed * 4 + r for r in (1, 2, 3))
+        # the loss launch's workspace belongs to this step (a captured graph keeps
+        # its pointer): grow-only, earlier buffers stay alive for graphs that hold them
+        self._loss_ws: Optional[torch.Tensor] = None
+        self._loss_ws_retired = []
         # fp64 accumulators, cleared without memset launches: the BN column sums of
         # the 3 tower calls (fwd + bwd) and the dbias slots live in ``arena``, which
         # clip+Adam zeroes as the step's last launch (with the grads it consumes);
@@ -169,18 +184,21 @@ class FusedTrainStep:
             else:
                 item_src, item_ids = torch.cat([pos_src, neg_src]), None
             # user tower and merged item tower: layer l of both in ONE launch
-            pq, u = chain_forward_pair((ib, item_src, item_ids, True, so, self.a_pqf, b),
-                                       (ub, user_src, user_ids, True, so, self.a_uf, 0), zero_buf=self.small)
+            pq, u = chain_forward_pair((ib, item_src, item_ids, True, so, self.a_pqf, b, self._sb_pos),
+                                       (ub, user_src, user_ids, True, so, self.a_uf, 0, self._sb_user),
+                                       zero_buf=self.small)
             p_out, q_out = pq.out[:b], pq.out[b:]
         else:
-            p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf, zero_buf=self.small)
-            q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf) \
-                if (neg_src is not None) else None
+            p = chain_forward(ib, pos_src, pos_ids, seed_offset=so, stats_arena=self.a_pf, zero_buf=self.small,
+                              seed_base=self._sb_pos)
+            q = chain_forward(ib, neg_src, neg_ids, seed_offset=so, stats_arena=self.a_nf,
+                              seed_base=self._sb_neg) if (neg_src is not None) else None
             p_out, q_out = p.out, (q.out if q is not None else None)
         if not merged:
             s_u.wait_stream(main)
             with torch.cuda.stream(s_u):
-                u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf)
+                u = chain_forward(ub, user_src, user_ids, seed_offset=so, stats_arena=self.a_uf,
+                                  seed_base=self._sb_user)
             main.wait_stream(s_u)
         d = u.out.shape[1]
         n_neg = (q_out.shape[0] // b) if q_out is not None else 0
@@ -191,7 +209,7 @@ class FusedTrainStep:
         else:
             dp = torch.empty_like(p_out)
             dq = torch.empty_like(q_out) if q_out is not None else None
-        ws = kernels.workspace(self.dev, native.lib().rt_twotower_loss_workspace_bytes(b, d), "loss")
+        ws = self._loss_workspace(native.lib().rt_twotower_loss_workspace_bytes(b, d))
         ubias, ibias = m.user_bias, m.item_bias
         with TIMER.region("loss_fwd_bwd", flops=6.0 * b * b * d + 6.0 * b * (n_neg + 1) * d,
                           bytes_=4.0 * d * (4 * b + 2 * b * n_neg)):
@@ -215,6 +233,16 @@ class FusedTrainStep:
                 chain_backward(ib, q, dq, slab, seed_offset=so, stats_arena=self.a_nb, attach=False)
             main.wait_stream(s_p)
         main.wait_stream(s_u)
+
+    def _loss_workspace(self, nbytes: int) -> torch.Tensor:
+        """This step's own loss workspace (a shared, growable
+        workspace could be swapped out from under a captured graph by any other
+        caller, e.g. a validation batch larger than the training batch)."""
+        if self._loss_ws is None or self._loss_ws.numel() < nbytes:
+            if self._loss_ws is not None:
+                self._loss_ws_retired.append(self._loss_ws)
+            self._loss_ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=self.dev)
+        return self._loss_ws
 
     def _allreduce(self):
         if self.pg is not None:  # data parallel: average the flat grad slab (one RCCL all-reduce)

@@ -138,29 +138,34 @@ def test_step_after_autograd_backward_matches_fresh_step(device):
     _check(m2, m1, [ref], [got])
 
 
-def test_feeder_graph_epoch_matches_eager(device):
-    """FeederGraph (batch rows at a device cursor, on-device negatives and the
-    fused step as one hipGraph per batch) reproduces the eager feeder-driven
-    loop: the same batches (ids compared exactly) and the same per-batch losses
-    (fp64 atomic reductions may reorder: 1e-5 relative). Dropout off: a
-    captured step draws its masks from the device counter with seeds fixed at
-    capture, an eager step from fresh host seeds (the mask contract itself is
-    tests/test_gpu_dropout.py)."""
+def _feeder_pair(device, dropout):
     from rtrec_amd.data.movielens import synthetic_movielens
     from rtrec_amd.training.datasets.movielens import DeviceFeeder
-    from rtrec_amd.training.fused_step import FeederGraph, FusedTrainStep
+    from rtrec_amd.training.fused_step import FusedTrainStep
     from rtrec_amd.training.utils import create_two_tower_model_for_training
     data = synthetic_movielens(seed=0)
     torch.manual_seed(7)
-    cfg = {"embedding_dim": 64, "hidden_layers": [256, 128], "dropout_rate": 0.0, "temperature": 0.05}
+    cfg = {"embedding_dim": 64, "hidden_layers": [256, 128], "dropout_rate": dropout, "temperature": 0.05}
     m1 = create_two_tower_model_for_training(3, 20, cfg)
     m2 = copy.deepcopy(m1)
     m1.to(device)
     m2.to(device)
     mk = lambda: DeviceFeeder(data.train_interactions, data.users, data.movies, num_negatives=16,  # noqa: E731
                               batch_size=256, device=device, seed=5)
-    fa, fb = mk(), mk()
-    sa, sb = FusedTrainStep(m1), FusedTrainStep(m2)
+    # the same dropout seed base: masks then depend only on the device step counter
+    return (m1, m2, mk(), mk(), FusedTrainStep(m1, dropout_seed=1234), FusedTrainStep(m2, dropout_seed=1234))
+
+
+def test_feeder_graph_epoch_matches_eager(device):
+    """FeederGraph (batch rows at a device cursor, on-device negatives and the
+    fused step as one hipGraph per batch) reproduces the eager feeder-driven
+    loop WITH dropout 0.2: the same batches (ids compared
+    exactly) and the same per-batch losses (fp64 atomic reductions may
+    reorder: 1e-5 relative). Eager and captured steps draw their masks from
+    the same per-chain seed bases plus the device step counter, so step t
+    masks agree whichever way the step runs."""
+    from rtrec_amd.training.fused_step import FeederGraph
+    m1, m2, fa, fb, sa, sb = _feeder_pair(device, 0.2)
     nb = 40
     eager, last = [], None
     for i, b in enumerate(fa):
@@ -177,3 +182,48 @@ def test_feeder_graph_epoch_matches_eager(device):
     np.testing.assert_allclose(got, np.asarray(eager), rtol=1e-5)
     for (k, v1), v2 in zip(m1.state_dict().items(), m2.state_dict().values()):
         assert torch.allclose(v1.float(), v2.float(), rtol=1e-4, atol=1e-5), k
+
+
+def test_dropout_masks_change_per_step_with_fixed_seed_base(device):
+    """A fixed seed base does not freeze the masks: consecutive steps on the
+    same batch with dropout on give different losses, and two step objects with
+    different seed bases differ at the same step."""
+    from rtrec_amd.training.fused_step import FusedTrainStep
+    m1, m2, fa, _, sa, _ = _feeder_pair(device, 0.2)
+    b = next(iter(fa))
+    args = (b["user_table"], b["item_table"], b["item_table"])
+    kw = dict(user_ids=b["user_ids"], pos_ids=b["pos_ids"], neg_ids=b["neg_ids"])
+    m3 = copy.deepcopy(m2)
+    s3 = FusedTrainStep(m3, dropout_seed=99)
+    l1 = float(sa(*args, **kw)[0].item())
+    l3 = float(s3(*args, **kw)[0].item())
+    assert l1 != l3
+    s0 = FusedTrainStep(copy.deepcopy(m2), dropout_seed=1234, lr=0.0)
+    la, lb = float(s0(*args, **kw)[0].item()), float(s0(*args, **kw)[0].item())
+    assert la != lb  # lr 0: the weights stay, only the step counter (and so the masks) moved
+
+
+def test_feeder_graph_survives_larger_validation_batch(device):
+    """a validation batch larger than the training batch
+    between two FeederGraph epochs grows the shared loss workspace of the
+    autograd path; the captured step owns its workspace, so the second epoch
+    still equals a twin run with no validation in between."""
+    from rtrec_amd.training.fused_step import FeederGraph
+    m1, m2, fa, fb, sa, sb = _feeder_pair(device, 0.0)
+    g1, g2 = FeederGraph(sa, fa), FeederGraph(sb, fb)
+    g1.run_epoch(max_batches=6)
+    g2.run_epoch(max_batches=6)
+    with torch.no_grad():  # the reference validate(): in-batch loss, eval mode, a 4x larger batch
+        m1.eval()
+        ut, mt = fa.user_table, fa.item_table
+        gen = torch.Generator(device=device).manual_seed(3)
+        u = m1.user_tower(ut[torch.randint(0, ut.shape[0], (1024,), device=device, generator=gen)])
+        p = m1.item_tower(mt[torch.randint(0, mt.shape[0], (1024,), device=device, generator=gen)])
+        float(m1.in_batch_negative_loss(u, p))
+        junk = [torch.full((1 << 20,), float("nan"), device=device) for _ in range(8)]  # reuse freed blocks
+        m1.train()
+    got = g1.run_epoch(max_batches=6).cpu().numpy()
+    want = g2.run_epoch(max_batches=6).cpu().numpy()
+    del junk
+    assert np.isfinite(got).all()
+    np.testing.assert_allclose(got, want, rtol=1e-5)
