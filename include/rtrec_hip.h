@@ -301,6 +301,19 @@ typedef struct {
     int prev_final;          /* prev_mode 1 only: 1 = the producing launch finalised the batch
                                 statistics (save_mean / save_invstd hold them; prev_stats, the
                                 running stats and num_batches_tracked are not touched here) */
+    /* Split-weight planes (DESIGN.md §5 note i): the three bf16 pieces (hi, mid, lo; split3) of a
+     * weight, computed ONCE per step by a side task of an earlier launch instead of in registers
+     * by every block that uses it. The pieces are the same bits split3 gives, so results are
+     * bit-identical to the in-register split. */
+    const uint16_t* w_planes;     /* optional [3][n][k] pieces of THIS launch's w (k % 8 == 0, n <= 128,
+                                     16-B aligned): the MFMA k-loop reads them (NULL = split w) */
+    uint16_t* wt_planes_out;      /* optional [3][k][n]: side task, the pieces of Wᵀ, read by the
+                                     backward's dz launch as rt_linear_bwd_args.wt_planes */
+    const float* next_w;          /* optional side task: the pieces of another weight [next_n][next_k]
+                                     (the next layer's w, for its launch's w_planes; next_k % 8 == 0) */
+    uint16_t* next_w_planes;      /* [3][next_n][next_k] */
+    int next_n;
+    int next_k;
 } rt_linear_fwd_args;
 
 int rt_linear_fwd_f32(const rt_linear_fwd_args* args, void* stream);
@@ -380,6 +393,9 @@ typedef struct {
     int64_t fold_words;
     int fold_splits;
     int fold_in;
+    const uint16_t* wt_planes; /* optional [3][k][n] split pieces of Wᵀ (rt_linear_fwd_args.wt_planes_out
+                                  of THIS step; n % 8 == 0, 16-B aligned): dA = dz·W reads them instead
+                                  of splitting wt / w in registers (bit-identical) */
 } rt_linear_bwd_args;
 
 int rt_linear_bwd_f32(const rt_linear_bwd_args* args, void* stream);

@@ -290,8 +290,11 @@ constexpr int FM = 32;  // rows per block
 
 __host__ __device__ __forceinline__ int pad8(int k) { return (k + 31) / 32 * 32; }  // k padded to whole 32-deep iterations
 
-template <int TPW, bool KVEC>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
+// WPL: the k-loop reads W's split pieces from rt_linear_fwd_args.w_planes
+// (TPW == 1, k % 8 == 0) instead of splitting W fragments in registers
+template <int TPW, bool KVEC, bool WPL>  // 32-col tiles per wave (n <= 128*TPW); KVEC: k % 4 == 0
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 3 : 2))) void linear_fwd_kernel(FwdLaunch L) {
+    static_assert(!WPL || (TPW == 1 && KVEC), "split-weight planes: one-tile waves, k % 4 == 0");
     const bool g1 = blockIdx.x >= L.split;
     const rt_linear_fwd_args& a = g1 ? L.a1 : L.a0;
     const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
@@ -354,6 +357,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
             }
         }
     }
+    // split-weight planes (side tasks, once per step instead of per block):
+    // the pieces of Wᵀ for the dz launch, and of the next layer's W for its
+    // forward launch — the same bits split3 gives in registers
+    if (a.wt_planes_out || a.next_w_planes) {
+        const int nblk = static_cast<int>(g1 ? gridDim.x - L.split : L.split);
+        if (a.wt_planes_out) {  // element (kk, nn) of Wᵀ = w[nn][kk]; 4 consecutive nn per thread
+            const int64_t plane = static_cast<int64_t>(n) * k;
+            const int nq = (n + 3) / 4;
+            for (int64_t e = static_cast<int64_t>(bid) * 256 + tid; e < static_cast<int64_t>(k) * nq;
+                 e += static_cast<int64_t>(nblk) * 256) {
+                const int kk = static_cast<int>(e / nq), n0 = static_cast<int>(e % nq) * 4;
+                float x[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[j] = n0 + j < n ? a.w[static_cast<int64_t>(n0 + j) * k + kk] : 0.f;
+                uint32_t h0, m0, l0, h1, m1, l1;
+                split3(x[0], x[1], h0, m0, l0);
+                split3(x[2], x[3], h1, m1, l1);
+                uint16_t* q = a.wt_planes_out + static_cast<int64_t>(kk) * n + n0;
+                if (n0 + 4 <= n && (n % 4) == 0) {
+                    *reinterpret_cast<uint2*>(q) = make_uint2(h0, h1);
+                    *reinterpret_cast<uint2*>(q + plane) = make_uint2(m0, m1);
+                    *reinterpret_cast<uint2*>(q + 2 * plane) = make_uint2(l0, l1);
+                } else {
+                    const uint32_t hv[2] = {h0, h1}, mv[2] = {m0, m1}, lv[2] = {l0, l1};
+                    for (int j = 0; j < 4 && n0 + j < n; ++j) {
+                        const int sh = 16 * (j & 1);
+                        q[j] = static_cast<uint16_t>(hv[j >> 1] >> sh);
+                        q[j + plane] = static_cast<uint16_t>(mv[j >> 1] >> sh);
+                        q[j + 2 * plane] = static_cast<uint16_t>(lv[j >> 1] >> sh);
+                    }
+                }
+            }
+        }
+        if (a.next_w_planes) {  // [next_n][next_k] row-major, next_k % 8 == 0: 8 elements per thread
+            const int64_t tot8 = static_cast<int64_t>(a.next_n) * a.next_k / 8;
+            const float4* src4 = reinterpret_cast<const float4*>(a.next_w);
+            s16x8* dst = reinterpret_cast<s16x8*>(a.next_w_planes);
+            for (int64_t e = static_cast<int64_t>(bid) * 256 + tid; e < tot8; e += static_cast<int64_t>(nblk) * 256) {
+                const float4 u = src4[2 * e], v = src4[2 * e + 1];
+                const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+                const Pieces pc = split8(x);
+                dst[e] = pc.hi;
+                dst[e + tot8] = pc.mid;
+                dst[e + 2 * tot8] = pc.lo;
+            }
+        }
+    }
     // one-tile waves (every C2 layer but the first) request their first W
     // fragments before the prologue (they do not depend on it), so the L2
     // latency hides behind the A-tile staging (wider waves would spill)
@@ -391,7 +441,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
                 dst[i][j] = v;
             }
     };
-    if constexpr (TPW == 1) load_w(0, wn);
+    // WPL: the k-block's three pieces straight from the planes (lane half h
+    // holds k = kb + 8h .. kb + 8h + 7 of k-block kb, 16 B per piece)
+    uint4 pv[2][3], pn[2][3];
+    const int64_t wplane = static_cast<int64_t>(n) * k;
+    auto load_p = [&](int s, uint4 (&dst)[2][3]) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int kk = s + 16 * b + 8 * h;
+            const bool ok = tile_on[0] && row_ok[0] && kk < k;
+            const uint16_t* q = a.w_planes + (static_cast<int64_t>(row_ok[0] ? w * 32 + c32 : 0) * k + (ok ? kk : 0));
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                dst[b][p] = ok ? *reinterpret_cast<const uint4*>(q + p * wplane) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    if constexpr (WPL) load_p(0, pn);
+    else if constexpr (TPW == 1) load_w(0, wn);
     float4 pre[8];
     if (early) {
         const int c = (tid % vpr) * 4, rstep = 256 / vpr, r0 = tid / vpr;
@@ -558,6 +624,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
     const uint16_t* ap = Ap + c32 * kp;
     const int asw = c32 & am;
     if constexpr (TPW != 1) load_w(0, wn);
+    if constexpr (WPL) {
+        for (int s = 0; s < kp; s += 32) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) pv[b][p] = pn[b][p];
+            if (s + 32 < kp) load_p(s + 32, pn);
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int ao = (((s + 16 * b) >> 3) + h) ^ asw;
+                Pieces pa;
+                pa.hi = *reinterpret_cast<const s16x8*>(ap + 8 * ao);
+                pa.mid = *reinterpret_cast<const s16x8*>(ap + aplane + 8 * ao);
+                pa.lo = *reinterpret_cast<const s16x8*>(ap + 2 * aplane + 8 * ao);
+                if (tile_on[0]) {
+                    const Pieces pb{__builtin_bit_cast(s16x8, pv[b][0]), __builtin_bit_cast(s16x8, pv[b][1]),
+                                    __builtin_bit_cast(s16x8, pv[b][2])};
+                    acc[0] = mfma3(pa, pb, acc[0]);
+                }
+            }
+        }
+    } else
     for (int s = 0; s < kp; s += 32) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i)
@@ -719,7 +807,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 // coalesced along k straight from L2 (the reduction runs over n).
 // (3 waves per SIMD: the C2 launches' 576 blocks need 3 co-resident blocks on
 // some CUs; the register cap moves the accumulators from AGPRs to VGPRs, no spill)
-template <int TPWK>  // 32-col dA tiles per wave (k <= 128*TPWK)
+// WPL: dA reads Wᵀ's split pieces from rt_linear_bwd_args.wt_planes (n % 8 == 0)
+template <int TPWK, bool WPL>  // 32-col dA tiles per wave (k <= 128*TPWK)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void linear_bwd_dz_kernel(BwdLaunch L) {
 #ifdef RT_FOLD_FIRST
     fold_side(L, 0);
@@ -778,8 +867,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             }
         }
     };
+    // WPL: per tile and k-block the three pieces of Wᵀ[kk][nn .. nn + 7], 16 B each
+    uint4 pv[TPWK][3], pn[TPWK][3];
+    const uint16_t* __restrict__ WtP = a.wt_planes;
+    const int64_t tplane = static_cast<int64_t>(k) * n;
+    auto load_p = [&](int s, uint4 (&dst)[TPWK][3]) {
+#pragma unroll
+        for (int i = 0; i < TPWK; ++i) {
+            const int kk = (w + 4 * i) * 32 + c32;
+            const int nn = s + 8 * h;
+            const bool ok = (w + 4 * i) * 32 < k && kk < k && nn < n;
+            const uint16_t* q = WtP + (ok ? static_cast<int64_t>(kk) * n + nn : 0);
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                dst[i][p] = ok ? *reinterpret_cast<const uint4*>(q + p * tplane) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
     if constexpr (TPWK == 1) {  // (two-tile waves would spill)
-        if (a.g_prev || a.dsrc) load_w(0, wn);
+        if (a.g_prev || a.dsrc) {
+            if constexpr (WPL) load_p(0, pn);
+            else load_w(0, wn);
+        }
     }
 
     // ---- phase A: dz tile ----
@@ -1063,6 +1171,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
 #pragma unroll
         for (int r = 0; r < 16; ++r) zpre[i][r] = ld ? zp[((r & 3) + 8 * (r >> 2)) * a.ld_src] : 0.f;
     }
+    if constexpr (WPL) {
+        if constexpr (TPWK != 1) load_p(0, pn);
+        for (int s = 0; s < np; s += 16) {
+#pragma unroll
+            for (int i = 0; i < TPWK; ++i)
+#pragma unroll
+                for (int p = 0; p < 3; ++p) pv[i][p] = pn[i][p];
+            if (s + 16 < np) load_p(s + 16, pn);
+            Pieces pa;
+            pa.hi = *reinterpret_cast<const s16x8*>(ap + s);
+            pa.mid = *reinterpret_cast<const s16x8*>(ap + plane + s);
+            pa.lo = *reinterpret_cast<const s16x8*>(ap + 2 * plane + s);
+#pragma unroll
+            for (int i = 0; i < TPWK; ++i) {
+                if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
+                const Pieces pb{__builtin_bit_cast(s16x8, pv[i][0]), __builtin_bit_cast(s16x8, pv[i][1]),
+                                __builtin_bit_cast(s16x8, pv[i][2])};
+                acc[i] = mfma3(pa, pb, acc[i]);
+            }
+        }
+    } else {
     if constexpr (TPWK != 1) load_w(0, wn);
     for (int s = 0; s < np; s += 16) {
 #pragma unroll
@@ -1079,6 +1208,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
             acc[i] = mfma3(pa, split8(wv[i]), acc[i]);
         }
+    }
     }
     RT_PP_MARK(2)
     const float pscale = a.prev_drop_p > 0.f ? 1.f / (1.f - a.prev_drop_p) : 1.f;
@@ -1593,6 +1723,13 @@ static int validate_fwd(const rt_linear_fwd_args* args) {
     if (a.fin_save_mean && (!a.stats_out || !a.fin_save_invstd || (!a.fin_running_mean != !a.fin_running_var)))
         return RT_ERR_INVALID;
     if (a.prev_final && (a.prev_mode != 1 || !a.save_mean || !a.save_invstd)) return RT_ERR_INVALID;
+    if (a.w_planes && ((a.k % 8) != 0 || a.n > 128 || (reinterpret_cast<uintptr_t>(a.w_planes) & 15) ||
+                       (reinterpret_cast<uintptr_t>(a.w) & 15)))
+        return RT_ERR_INVALID;
+    if (a.next_w_planes && (!a.next_w || a.next_n <= 0 || a.next_k <= 0 || (a.next_k % 8) != 0 ||
+                            (reinterpret_cast<uintptr_t>(a.next_w) & 15) ||
+                            (reinterpret_cast<uintptr_t>(a.next_w_planes) & 15)))
+        return RT_ERR_INVALID;
     const int kp = mlp::pad8(a.k);
     const int tpw = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
     const size_t lds = (2 * kp + 3 * mlp::FM * kp / 2 + 4 * tpw * mlp::FM) * sizeof(float) + mlp::FM * sizeof(int64_t) + 16;
@@ -1608,12 +1745,13 @@ extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_arg
     args = noa;
 #endif
     int tpw = 1, kp_max = 0;
-    bool kvec = true;
+    bool kvec = true, wpl = true;  // wpl: every argument set brings its W planes
     unsigned blocks[2] = {0u, 0u};
     for (int g = 0; g < n_args; ++g) {
         const int v = validate_fwd(&args[g]);
         if (v) return v;
         const rt_linear_fwd_args& a = args[g];
+        wpl = wpl && a.w_planes != nullptr;
         const int t = a.n <= 128 ? 1 : a.n <= 256 ? 2 : 4;
         tpw = t > tpw ? t : tpw;
         kvec = kvec && (a.k % 4) == 0 && (reinterpret_cast<uintptr_t>(a.w) & 15) == 0;
@@ -1633,15 +1771,17 @@ extern "C" int rt_linear_fwd_f32_multi(const rt_linear_fwd_args* args, int n_arg
     if (total == 0) return RT_OK;
     hipStream_t st = as_stream(stream);
     const dim3 grid(total);
-#define RT_FWD(T, V)                                                                              \
+#define RT_FWD(T, V, P)                                                                           \
     do {                                                                                          \
-        allow_lds(mlp::linear_fwd_kernel<T, V>, lds);                                             \
-        hipLaunchKernelGGL((mlp::linear_fwd_kernel<T, V>), grid, dim3(256), lds, st, L);          \
+        allow_lds(mlp::linear_fwd_kernel<T, V, P>, lds);                                          \
+        hipLaunchKernelGGL((mlp::linear_fwd_kernel<T, V, P>), grid, dim3(256), lds, st, L);       \
     } while (0)
-    if (kvec) {
-        if (tpw == 1) RT_FWD(1, true); else if (tpw == 2) RT_FWD(2, true); else RT_FWD(4, true);
+    if (kvec && tpw == 1 && wpl) {
+        RT_FWD(1, true, true);
+    } else if (kvec) {
+        if (tpw == 1) RT_FWD(1, true, false); else if (tpw == 2) RT_FWD(2, true, false); else RT_FWD(4, true, false);
     } else {
-        if (tpw == 1) RT_FWD(1, false); else if (tpw == 2) RT_FWD(2, false); else RT_FWD(4, false);
+        if (tpw == 1) RT_FWD(1, false, false); else if (tpw == 2) RT_FWD(2, false, false); else RT_FWD(4, false, false);
     }
 #undef RT_FWD
     return check_launch("linear_fwd_kernel");
@@ -1688,6 +1828,7 @@ static int validate_bwd(const rt_linear_bwd_args* args) {
     if (a.fold_src && (!a.fold_dst || a.fold_words % 4 != 0 || a.fold_splits <= 0 || a.fold_in < 0 || a.fold_in > 1 ||
                        (reinterpret_cast<uintptr_t>(a.fold_src) & 15) || (reinterpret_cast<uintptr_t>(a.fold_dst) & 15)))
         return RT_ERR_INVALID;
+    if (a.wt_planes && ((a.n % 8) != 0 || (reinterpret_cast<uintptr_t>(a.wt_planes) & 15))) return RT_ERR_INVALID;
     return RT_OK;
 }
 
@@ -1696,11 +1837,13 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
     int tpwk = 1;
     size_t lds = 0;
     unsigned blocks[2] = {0u, 0u};
+    bool wpl = true;  // every argument set with a dA brings Wᵀ's planes
     for (int g = 0; g < n_args; ++g) {
         const int v = validate_bwd(&args[g]);
         if (v) return v;
         const rt_linear_bwd_args& a = args[g];
         const bool need_da = a.g_prev || a.dsrc;
+        wpl = wpl && (!need_da || a.wt_planes != nullptr);
         const int t = !need_da ? 1 : a.k <= 128 ? 1 : a.k <= 256 ? 2 : 4;
         tpwk = t > tpwk ? t : tpwk;
         const int np = mlp::pad8(a.n);
@@ -1723,11 +1866,17 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
     if (total == 0) return RT_OK;
     const dim3 grid(total);
     hipStream_t st = as_stream(stream);
+#define RT_DZ(T, P)                                                                           \
+    do {                                                                                      \
+        allow_lds(mlp::linear_bwd_dz_kernel<T, P>, lds);                                      \
+        hipLaunchKernelGGL((mlp::linear_bwd_dz_kernel<T, P>), grid, dim3(256), lds, st, L);   \
+    } while (0)
     switch (tpwk) {
-        case 1: allow_lds(mlp::linear_bwd_dz_kernel<1>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<1>, grid, dim3(256), lds, st, L); break;
-        case 2: allow_lds(mlp::linear_bwd_dz_kernel<2>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<2>, grid, dim3(256), lds, st, L); break;
-        default: allow_lds(mlp::linear_bwd_dz_kernel<4>, lds); hipLaunchKernelGGL(mlp::linear_bwd_dz_kernel<4>, grid, dim3(256), lds, st, L); break;
+        case 1: if (wpl) RT_DZ(1, true); else RT_DZ(1, false); break;
+        case 2: if (wpl) RT_DZ(2, true); else RT_DZ(2, false); break;
+        default: RT_DZ(4, false); break;
     }
+#undef RT_DZ
     return check_launch("linear_bwd_dz_kernel");
 }
 

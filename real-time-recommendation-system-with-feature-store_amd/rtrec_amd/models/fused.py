@@ -203,6 +203,10 @@ class ChainCtx:
     normalize: bool = True
     seg_split: int = 0  # > 0: rows [0, seg_split) and [seg_split, m) are separate BN batches
     wts: List[Optional[torch.Tensor]] = field(default_factory=list)  # Wᵀ of each Linear (fwd writes, dz reads)
+    # split pieces of each Linear's W ([3][n][k] bf16: the previous launch writes, the
+    # Linear's own forward reads) and of its Wᵀ ([3][k][n]: the forward writes, dz reads)
+    w_planes: List[Optional[torch.Tensor]] = field(default_factory=list)
+    wt_planes: List[Optional[torch.Tensor]] = field(default_factory=list)
     ains: List[Optional[torch.Tensor]] = field(default_factory=list)  # transformed inputs (fwd writes, dW reads)
 
 
@@ -224,6 +228,12 @@ DBIAS_ROWS = STAT_SLOTS + 1
 # cost more — C2 step 0.2392 -> 0.2505 ms in a same-box A/B
 # (profiles/r05_c2_ab_bn_final.txt). RTREC_BN_FINAL=1 turns it on.
 FINALIZE_BN_IN_PRODUCER = os.environ.get("RTREC_BN_FINAL", "0") == "1"
+# Split-weight planes (DESIGN.md §5 note i): each weight's three bf16 pieces are
+# written once per chain by a side task of the launch before the one that uses
+# them (rt_linear_fwd_args.next_w_planes for the forward's k-loop, wt_planes_out
+# for the dz launch's dA) instead of being split in registers by every block.
+# Bit-identical either way. RTREC_W_PLANES=0 turns it off (A/B).
+SPLIT_W_PLANES = os.environ.get("RTREC_W_PLANES", "1") != "0"
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
@@ -386,12 +396,29 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         a.act = b.act
         # Wᵀ of this Linear for its backward's dA (layers past the first: their
         # dz launch computes the previous block's gradient); training forwards
-        # only — eval / serving forwards have no backward to read it
-        wt = torch.empty((lin.in_features, lin.out_features), dtype=torch.float32, device=dev) \
-            if li > 0 and lin.training else None
-        if wt is not None:
-            a.wt_out = wt.data_ptr()
+        # only — eval / serving forwards have no backward to read it. With
+        # SPLIT_W_PLANES the forward writes Wᵀ's split pieces instead (n % 8 == 0).
+        wt = wtp = None
+        if li > 0 and lin.training:
+            if SPLIT_W_PLANES and lin.out_features % 8 == 0:
+                wtp = torch.empty((3, lin.in_features, lin.out_features), dtype=torch.int16, device=dev)
+                a.wt_planes_out = wtp.data_ptr()
+            else:
+                wt = torch.empty((lin.in_features, lin.out_features), dtype=torch.float32, device=dev)
+                a.wt_out = wt.data_ptr()
         ctx.wts.append(wt)
+        ctx.wt_planes.append(wtp)
+        # W's split pieces for this launch's k-loop, written by the previous
+        # launch of the chain (layers past the first; k % 8 == 0, n <= 128)
+        wp = None
+        if SPLIT_W_PLANES and li > 0 and lin.in_features % 8 == 0 and lin.out_features <= 128:
+            wp = torch.empty((3, lin.out_features, lin.in_features), dtype=torch.int16, device=dev)
+            prev = layers[li - 1]
+            prev.next_w = lin.weight.data_ptr()
+            prev.next_w_planes = wp.data_ptr()
+            prev.next_n, prev.next_k = lin.out_features, lin.in_features
+            a.w_planes = wp.data_ptr()
+        ctx.w_planes.append(wp)
         # training: the launch also writes the transformed input it stages (act →
         # BN → dropout of the previous block), which this Linear's dW launch then
         # reads as is instead of recomputing it (rt_linear_fwd_args.a_out / a_in)
@@ -606,6 +633,8 @@ def _backward_plan(blocks: List[Block], ctx: ChainCtx, dout: torch.Tensor, slab:
             a.g_prev = g.data_ptr()
             if li < len(ctx.wts) and ctx.wts[li] is not None:
                 a.wt = ctx.wts[li].data_ptr()
+            if li < len(ctx.wt_planes) and ctx.wt_planes[li] is not None:
+                a.wt_planes = ctx.wt_planes[li].data_ptr()
             if li < len(ctx.ains) and ctx.ains[li] is not None:
                 a.a_in = ctx.ains[li].data_ptr()
         layers.append(a)

@@ -53,6 +53,8 @@ class LinearFwdArgs(ctypes.Structure):
         ("wt_out", vp), ("a_out", vp),
         ("fin_save_mean", vp), ("fin_save_invstd", vp), ("fin_running_mean", vp), ("fin_running_var", vp),
         ("fin_num_batches_tracked", vp), ("fin_eps", c_f32), ("fin_momentum", c_f32), ("prev_final", c_int),
+        ("w_planes", vp), ("wt_planes_out", vp), ("next_w", vp), ("next_w_planes", vp), ("next_n", c_int),
+        ("next_k", c_int),
     ]
 
 
@@ -68,6 +70,7 @@ class LinearBwdArgs(ctypes.Structure):
         ("seed_offset", vp), ("g_prev", vp), ("g_prev_stats", vp), ("dsrc", vp), ("seg_split", c_i64),
         ("dbias_slots", vp), ("wt", vp), ("fuse_dz", c_int), ("a_in", vp), ("dw_part", vp),
         ("fold_src", vp), ("fold_dst", vp), ("fold_words", c_i64), ("fold_splits", c_int), ("fold_in", c_int),
+        ("wt_planes", vp),
     ]
 
 

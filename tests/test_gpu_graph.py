@@ -180,8 +180,14 @@ def test_feeder_graph_epoch_matches_eager(device):
     assert torch.equal(fg.users, last["user_ids"]) and torch.equal(fg.pos, last["pos_ids"])
     assert torch.equal(fg.neg, last["neg_ids"])
     np.testing.assert_allclose(got, np.asarray(eager), rtol=1e-5)
+    # weights after 40 Adam steps: the last dW launch adds its tiles with fp32
+    # atomics, so eager and replayed steps sum in different orders; Adam's
+    # normalised update turns a last-bit difference of a near-zero gradient
+    # into up to lr per step. Bar: half an Adam step (lr = 1e-3), while the
+    # losses above agree to 1e-5 relative at every step.
     for (k, v1), v2 in zip(m1.state_dict().items(), m2.state_dict().values()):
-        assert torch.allclose(v1.float(), v2.float(), rtol=1e-4, atol=1e-5), k
+        diff = float((v1.float() - v2.float()).abs().max()) if v1.numel() else 0.0
+        assert diff <= 5e-4, (k, diff)
 
 
 def test_dropout_masks_change_per_step_with_fixed_seed_base(device):

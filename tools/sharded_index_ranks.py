@@ -30,7 +30,7 @@ def main(out_path):
     from rtrec_amd.dist import sharded as sh
     from rtrec_amd.serving.retrieval import HipFlatIPIndex, RetrievalEngine
     rng = np.random.default_rng(17)
-    n, d, nq, k = 65_536 * world + 4099, 128, 1536, 100
+    n, d, nq, k = 65_536 * world + 4099, 128, 8192, 100  # >= 7,681 queries: the v4 plan
     corpus = (rng.integers(-8, 9, size=(n, d)) / 64.0).astype(np.float32)
     corpus[n - 1] = corpus[5]
     corpus[n // 2 + 1] = corpus[7]
@@ -57,7 +57,8 @@ def main(out_path):
 
     check("search k=100", queries, k)
     check("search k=10", queries[:777], 10)
-    check("filter_ids", queries[:300], 20, ids[::4])
+    check("filter_ids", queries, 20, ids[::4])        # k_search 40: the global path
+    check("filter_ids small batch", queries[:300], 20, ids[::4])
     extra = (rng.integers(-8, 9, size=(3001, d)) / 64.0).astype(np.float32)
     extra[0] = corpus[5]
     eng.update_index(extra, [f"x{j}" for j in range(3001)])
@@ -78,7 +79,7 @@ def main(out_path):
         ops.rank = lambda kk, s, t: 1
         return ops
     eng.index._ops = forced
-    check("forced rescue", queries[:256], k)
+    check("forced rescue", queries, k)
     eng.index._ops = real
     report["ok"] = all(c["ok"] for c in report["checks"])
     with open(f"{out_path}.rank{rank}", "w") as f:
