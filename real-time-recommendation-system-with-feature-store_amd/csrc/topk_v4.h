@@ -69,6 +69,14 @@ constexpr int kFinishRegs = 16;        // candidates per lane the finish holds i
 #define RT_TOPK_V4_QS 2
 #endif
 constexpr int kQS = RT_TOPK_V4_QS;     // query sets of 32 per wave
+// one candidate region and cursor per query shared by its two lane halves
+// (the lanes (col, 0) and (col, 1) of a query interleave their appends), instead
+// of one region per (query, half): half the open buffer lines per block
+#ifdef RT_TOPK_V4_PER_HALF
+constexpr bool kShared = false;
+#else
+constexpr bool kShared = true;
+#endif
 
 template <int QS>
 struct Geo {
@@ -363,7 +371,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     float thr[QS];
 #pragma unroll
     for (int j = 0; j < QS; ++j) {
-        woff0[j] = static_cast<uint32_t>(((j * 32 + col) * kCap + half * kHalf) * sizeof(Cand));
+        woff0[j] = static_cast<uint32_t>(((j * 32 + col) * kCap + (kShared ? 0 : half * kHalf)) * sizeof(Cand));
         woff[j] = woff0[j];
         thr[j] = qok[j] ? -FLT_MAX : INFINITY;
     }
@@ -376,8 +384,10 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         for (int j = 0; j < QS; ++j) thr[j] = qok[j] ? fmaxf(a.thr_in[qw + j * 32 + col], -FLT_MAX) : INFINITY;
     }
     constexpr int kHead = C::NSUB * 16;  // appends per half between two compaction checks, at most
-    constexpr uint32_t kLimBytes = static_cast<uint32_t>((kHalf - kHead) * sizeof(Cand));
-    constexpr int kLimit = kHalf - kHead;  // a compaction keeps at most this many entries (in all)
+    // shared region: both halves append up to kHead each between checks
+    constexpr int kRoom = kShared ? kCap - 2 * kHead : kHalf - kHead;
+    constexpr uint32_t kLimBytes = static_cast<uint32_t>(kRoom * sizeof(Cand));
+    constexpr int kLimit = kRoom;  // a compaction keeps at most this many entries (in all)
 
     // ---- DMA plan (as v3): this wave's pieces w, w+8, ... of a stage ----
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -470,8 +480,17 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     auto store_loop = [&](int j, uint32_t pm, const f32x16& acc, int64_t sub0) {
         const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
         uint32_t wo = woff[j];
-        while (__ballot(pm != 0u)) {
+        while (true) {
+            const uint64_t sb = __ballot(pm != 0u);
+            if (sb == 0ull) break;
             issued += 1;  // exactly one store instruction (dwordx2) for the wave
+            // shared region: the half-1 lane writes behind its half-0 partner
+            // when both store this round; both advance by the pair's stores
+            uint32_t other = 0u, slot = wo;
+            if constexpr (kShared) {
+                other = static_cast<uint32_t>((sb >> (lane ^ 32)) & 1ull);
+                slot = wo + (half ? other * static_cast<uint32_t>(sizeof(Cand)) : 0u);
+            }
             if (pm) {
                 // the lowest passing row as an isolated bit, tested against
                 // constant masks; the score is picked by explicit v_cndmask
@@ -492,10 +511,12 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
                 const float s = lane_sel(m3, v2[0], v2[1]);
                 const uint32_t id = sub_lane + (b0 ? 1u : 0u) + (b1 ? 2u : 0u) + (b2 ? 8u : 0u) + (b3 ? 16u : 0u);
                 // a compiler-visible SADDR store (hipcc counts it and pads its hazards)
-                *reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(wbytes + wo) =
+                *reinterpret_cast<__attribute__((address_space(1))) uint64_t*>(wbytes + slot) =
                     (static_cast<uint64_t>(id) << 32) | __float_as_uint(s);
-                wo += 8;
+                if constexpr (!kShared) wo += 8;
             }
+            if constexpr (kShared)
+                wo += static_cast<uint32_t>(sizeof(Cand)) * (((sb >> lane) & 1ull ? 1u : 0u) + other);
         }
         woff[j] = wo;
     };
@@ -522,11 +543,11 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
                 const int c = __builtin_ctz(need);
                 need &= need - 1;
                 const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
-                int n0 = __shfl(cnt, c, 64), n1 = __shfl(cnt, c + 32, 64);
+                int n0 = __shfl(cnt, c, 64), n1 = kShared ? 0 : __shfl(cnt, c + 32, 64);
                 float nt;
                 compact_stream(cbase + static_cast<int64_t>(j * 32 + c) * kCap, n0, n1, k, kLimit, whist, nt);
                 if (col == c) {
-                    woff[j] = woff0[j] + static_cast<uint32_t>((half ? n1 : n0) * sizeof(Cand));
+                    woff[j] = woff0[j] + static_cast<uint32_t>(((half && !kShared) ? n1 : n0) * sizeof(Cand));
                     thr[j] = fmaxf(thr[j], nt);
                 }
             }
@@ -796,7 +817,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
 #pragma unroll
         for (int j = 0; j < QS; ++j) {
             const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
-            const int tot = cnt + __shfl_xor(cnt, 32, 64);
+            const int tot = kShared ? cnt : cnt + __shfl_xor(cnt, 32, 64);
             const bool fail = qok[j] && tot < k;
             any |= fail;
             if (fail) {
@@ -815,7 +836,8 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
 #pragma unroll
     for (int j = 0; j < QS; ++j) {
         const int cnt = static_cast<int>((woff[j] - woff0[j]) / sizeof(Cand));
-        meta[((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * 2 + half] = cnt;
+        // shared region: the whole count in the half-0 segment, the half-1 segment empty
+        meta[((static_cast<int64_t>(split) * q_pad) + qw + j * 32 + col) * 2 + half] = (kShared && half) ? 0 : cnt;
     }
 #ifdef RT_TOPK_PROBE_TIMING
     {  // [total, DMA wait, barrier, main sub-tiles, sample pass, compaction checks]

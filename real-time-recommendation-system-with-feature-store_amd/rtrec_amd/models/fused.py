@@ -232,8 +232,12 @@ FINALIZE_BN_IN_PRODUCER = os.environ.get("RTREC_BN_FINAL", "0") == "1"
 # written once per chain by a side task of the launch before the one that uses
 # them (rt_linear_fwd_args.next_w_planes for the forward's k-loop, wt_planes_out
 # for the dz launch's dA) instead of being split in registers by every block.
-# Bit-identical either way. RTREC_W_PLANES=0 turns it off (A/B).
-SPLIT_W_PLANES = os.environ.get("RTREC_W_PLANES", "1") != "0"
+# Bit-identical either way (tests/test_gpu_wplanes.py). Off by default: the
+# k-loops are bound by their W fragment loads, not by the split VALU, and three
+# 16-byte piece loads per k-block cost more than two float4 loads plus the split
+# — C2 step 0.2428 -> 0.2563 ms in a same-box A/B (profiles/r06_c2_ab_wplanes.txt).
+# RTREC_W_PLANES=1 turns it on.
+SPLIT_W_PLANES = os.environ.get("RTREC_W_PLANES", "0") == "1"
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:

@@ -160,10 +160,9 @@ def test_feeder_graph_epoch_matches_eager(device):
     """FeederGraph (batch rows at a device cursor, on-device negatives and the
     fused step as one hipGraph per batch) reproduces the eager feeder-driven
     loop WITH dropout 0.2: the same batches (ids compared
-    exactly) and the same per-batch losses (fp64 atomic reductions may
-    reorder: 1e-5 relative). Eager and captured steps draw their masks from
-    the same per-chain seed bases plus the device step counter, so step t
-    masks agree whichever way the step runs."""
+    exactly) and the same per-batch losses. Eager and captured steps draw
+    their masks from the same per-chain seed bases plus the device step
+    counter, so step t masks agree whichever way the step runs."""
     from rtrec_amd.training.fused_step import FeederGraph
     m1, m2, fa, fb, sa, sb = _feeder_pair(device, 0.2)
     nb = 40
@@ -179,15 +178,20 @@ def test_feeder_graph_epoch_matches_eager(device):
     assert fb.epoch == 1
     assert torch.equal(fg.users, last["user_ids"]) and torch.equal(fg.pos, last["pos_ids"])
     assert torch.equal(fg.neg, last["neg_ids"])
-    np.testing.assert_allclose(got, np.asarray(eager), rtol=1e-5)
-    # weights after 40 Adam steps: the last dW launch adds its tiles with fp32
-    # atomics, so eager and replayed steps sum in different orders; Adam's
-    # normalised update turns a last-bit difference of a near-zero gradient
-    # into up to lr per step. Bar: half an Adam step (lr = 1e-3), while the
-    # losses above agree to 1e-5 relative at every step.
+    # The last dW launch of a step adds its tiles with fp32 atomics, so two runs
+    # of the SAME eager loop already differ in the last bits of some gradients,
+    # and Adam's normalised update plus dropout amplify that over the epoch:
+    # measured on the GPU (profiles/r06_dropout_determinism.txt, 40 steps at
+    # p = 0.2) eager vs eager 4.6e-5 loss relative / 2.1e-3 max weight, eager vs
+    # graph 2.3e-5 / 6.0e-4 (p = 0: 5e-8 / 2e-6). A mask mismatch moves the
+    # loss by ~1e-2 at the first step. Bars: the first 5 steps within 1e-5
+    # relative, every step within 2e-4, weights within 5e-3 (vs ~1.4 moved).
+    eager = np.asarray(eager)
+    np.testing.assert_allclose(got[:5], eager[:5], rtol=1e-5)
+    np.testing.assert_allclose(got, eager, rtol=2e-4)
     for (k, v1), v2 in zip(m1.state_dict().items(), m2.state_dict().values()):
         diff = float((v1.float() - v2.float()).abs().max()) if v1.numel() else 0.0
-        assert diff <= 5e-4, (k, diff)
+        assert diff <= 5e-3, (k, diff)
 
 
 def test_dropout_masks_change_per_step_with_fixed_seed_base(device):
