@@ -207,7 +207,8 @@ def test_dropout_masks_change_per_step_with_fixed_seed_base(device):
     s3 = FusedTrainStep(m3, dropout_seed=99)
     l1 = float(sa(*args, **kw)[0].item())
     l3 = float(s3(*args, **kw)[0].item())
-    assert l1 != l3
+    # other masks move the first-step loss far beyond the 1e-5 bar of the graph test
+    assert abs(l1 - l3) > 1e-4 * abs(l1), (l1, l3)
     s0 = FusedTrainStep(copy.deepcopy(m2), dropout_seed=1234, lr=0.0)
     la, lb = float(s0(*args, **kw)[0].item()), float(s0(*args, **kw)[0].item())
     assert la != lb  # lr 0: the weights stay, only the step counter (and so the masks) moved
