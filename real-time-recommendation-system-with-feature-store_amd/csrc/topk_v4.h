@@ -477,6 +477,9 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
         }
         return pm;
     };
+#ifdef RT_TOPK_V4_STREAMTEST
+    uint32_t scur = 0u;
+#endif
     auto store_loop = [&](int j, uint32_t pm, const f32x16& acc, int64_t sub0) {
         const uint32_t sub_lane = static_cast<uint32_t>(sub0) + static_cast<uint32_t>(4 * half);
         uint32_t wo = woff[j];
@@ -491,6 +494,12 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
                 other = static_cast<uint32_t>((sb >> (lane ^ 32)) & 1ull);
                 slot = wo + (half ? other * static_cast<uint32_t>(sizeof(Cand)) : 0u);
             }
+#ifdef RT_TOPK_V4_STREAMTEST  // timing probe only: wave-contiguous appends (the finish reads garbage)
+            slot = ((scur + __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(sb >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(sb), 0u))) &
+                    (64u * kCap - 1u)) * static_cast<uint32_t>(sizeof(Cand));
+            scur += static_cast<uint32_t>(__popcll(sb));
+#endif
             if (pm) {
                 // the lowest passing row as an isolated bit, tested against
                 // constant masks; the score is picked by explicit v_cndmask
