@@ -41,6 +41,7 @@ struct BwdLaunch {
     unsigned tn0, tk0, tn1, tk1;  // dW: tile grid of each group
     bool vec0, vec1;              // dW: float4 staging loads
     int ngroups;                  // argument sets in this launch (a1 is a copy of a0 when 1)
+    unsigned ksplit = 1;          // dz: blocks per row block (dA column parts)
 };
 
 // Side task of a dz (which = 0) or dW (which = 1) launch: fold an EARLIER dW
@@ -808,14 +809,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TPW == 1 ? 
 // (3 waves per SIMD: the C2 launches' 576 blocks need 3 co-resident blocks on
 // some CUs; the register cap moves the accumulators from AGPRs to VGPRs, no spill)
 // WPL: dA reads Wᵀ's split pieces from rt_linear_bwd_args.wt_planes (n % 8 == 0)
-template <int TPWK, bool WPL>  // 32-col dA tiles per wave (k <= 128*TPWK)
+// KS: L.ksplit > 1 (dA columns of a row block split over blocks)
+template <int TPWK, bool WPL, bool KS>  // 32-col dA tiles per wave (k <= 128*TPWK)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void linear_bwd_dz_kernel(BwdLaunch L) {
 #ifdef RT_FOLD_FIRST
     fold_side(L, 0);
 #endif
-    const bool g1 = blockIdx.x >= L.split;
+    // L.ksplit > 1: the dA columns of a row block are split over ksplit blocks
+    // (part kpart takes dA tiles kpart·4·TPWK ..), so a launch with fewer row
+    // blocks than CUs still fills the chip; phase A's side effects (dz_ws, the
+    // dbias slots, dgamma/dbeta) belong to part 0
+    const unsigned kpart = KS ? blockIdx.x % L.ksplit : 0u, bx = KS ? blockIdx.x / L.ksplit : blockIdx.x;
+    const bool prim = kpart == 0;
+    const int tb = static_cast<int>(kpart) * 4 * TPWK;  // first dA column tile of this block
+    const bool g1 = bx >= L.split;
     const rt_linear_bwd_args& a = g1 ? L.a1 : L.a0;
-    const unsigned bid = blockIdx.x - (g1 ? L.split : 0u);
+    const unsigned bid = bx - (g1 ? L.split : 0u);
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const int n = a.n, k = a.k;
     const int64_t m = a.m;
@@ -846,8 +855,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     auto load_w = [&](int s, float (&dst)[TPWK][8]) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
-            const int kk = (w + 4 * i) * 32 + c32;
-            const bool on = (w + 4 * i) * 32 < k && kk < k;
+            const int kk = (tb + w + 4 * i) * 32 + c32;
+            const bool on = (tb + w + 4 * i) * 32 < k && kk < k;
             if (WtT) {
                 const int nn = s + 8 * h;
                 float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
@@ -874,9 +883,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     auto load_p = [&](int s, uint4 (&dst)[TPWK][3]) {
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
-            const int kk = (w + 4 * i) * 32 + c32;
+            const int kk = (tb + w + 4 * i) * 32 + c32;
             const int nn = s + 8 * h;
-            const bool ok = (w + 4 * i) * 32 < k && kk < k && nn < n;
+            const bool ok = (tb + w + 4 * i) * 32 < k && kk < k && nn < n;
             const uint16_t* q = WtP + (ok ? static_cast<int64_t>(kk) * n + nn : 0);
 #pragma unroll
             for (int p = 0; p < 3; ++p)
@@ -926,7 +935,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                 d.y = big ? (dv[p].y - lv[p].y * dot) * inv : dv[p].y * inv;
                 d.z = big ? (dv[p].z - lv[p].z * dot) * inv : dv[p].z * inv;
                 d.w = big ? (dv[p].w - lv[p].w * dot) * inv : dv[p].w * inv;
-                st_act4(a.dz_ws + gr * n + c, d);
+                if (prim) st_act4(a.dz_ws + gr * n + c, d);
             }
             *reinterpret_cast<float4*>(Dz + r * ldz + c) = d;
         }
@@ -945,7 +954,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                     if (c < n) {
                         const float dv = a.dout[gr * n + c];
                         dz = big ? (dv - a.l2_out[gr * n + c] * dot) * inv : dv * inv;
-                        a.dz_ws[gr * n + c] = dz;
+                        if (prim) a.dz_ws[gr * n + c] = dz;
                     }
                     Dz[rr * ldz + c] = dz;
                 }
@@ -1038,7 +1047,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                     d.w = one(gv[u].w, zv[u].w, fA.w, fB.w, fC.w, fM.w, fI.w);
                     if (gr >= m || c >= n) d = make_float4(0.f, 0.f, 0.f, 0.f);
                     *reinterpret_cast<float4*>(Dz + r * ldz + c) = d;
-                    if (gr < m && c < n) st_act4(a.dz_ws + gr * n + c, d);
+                    if (prim && gr < m && c < n) st_act4(a.dz_ws + gr * n + c, d);
                 }
             }
         } else
@@ -1087,7 +1096,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
                     dzv[j] = dz;
                 }
                 *reinterpret_cast<float4*>(Dz + r * ldz + c) = make_float4(dzv[0], dzv[1], dzv[2], dzv[3]);
-                if (gr < m && c < n) {
+                if (prim && gr < m && c < n) {
                     const int64_t off = gr * n + c;
                     if (vec) *reinterpret_cast<float4*>(a.dz_ws + off) = make_float4(dzv[0], dzv[1], dzv[2], dzv[3]);
                     else
@@ -1097,7 +1106,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
         }
     }
     RT_PP_MARK(0)
-    if (a.dbias && a.dbias_slots) {
+    if (prim && a.dbias && a.dbias_slots) {
         // dbias partials: this block's column sums of dz into fp64 slot bid % SLOTS
         // (the dW launch folds the slots; contention per address = blocks / SLOTS)
         __syncthreads();
@@ -1109,7 +1118,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             atomicAdd(&sl[c], static_cast<double>(cs));
         }
     }
-    if (bid == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
+    if (prim && bid == 0 && (a.grad_mode == 1 || a.grad_mode == 2) && a.dgamma) {
         // dgamma/dbeta of each BN batch (segment), summed like two tower calls' grads
         for (int c = tid; c < n; c += 256) {
             for (int sg = 0; sg < (two ? 2 : 1); ++sg) {
@@ -1163,7 +1172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     float zpre[TPWK][16], pmean[TPWK], pinv[TPWK];
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
-        const int kk = (w + 4 * i) * 32 + c32;
+        const int kk = (tb + w + 4 * i) * 32 + c32;
         const bool ld = fast && want_stats && kk < k;
         pmean[i] = ld ? a.prev_mean[my_seg * k + kk] : 0.f;
         pinv[i] = ld ? a.prev_invstd[my_seg * k + kk] : 0.f;
@@ -1185,7 +1194,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
             pa.lo = *reinterpret_cast<const s16x8*>(ap + 2 * plane + s);
 #pragma unroll
             for (int i = 0; i < TPWK; ++i) {
-                if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
+                if ((tb + w + 4 * i) * 32 >= k) continue;  // wave-uniform
                 const Pieces pb{__builtin_bit_cast(s16x8, pv[i][0]), __builtin_bit_cast(s16x8, pv[i][1]),
                                 __builtin_bit_cast(s16x8, pv[i][2])};
                 acc[i] = mfma3(pa, pb, acc[i]);
@@ -1205,7 +1214,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
         pa.lo = *reinterpret_cast<const s16x8*>(ap + 2 * plane + s);
 #pragma unroll
         for (int i = 0; i < TPWK; ++i) {
-            if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform
+            if ((tb + w + 4 * i) * 32 >= k) continue;  // wave-uniform
             acc[i] = mfma3(pa, split8(wv[i]), acc[i]);
         }
     }
@@ -1218,10 +1227,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void l
     const float psl = act_slope(a.prev_act);
 #pragma unroll
     for (int i = 0; i < TPWK; ++i) {
-        const int kk = (w + 4 * i) * 32 + c32;
+        const int kk = (tb + w + 4 * i) * 32 + c32;
         const bool col_ok = kk < k;
         float s1 = 0.f, s2 = 0.f;
-        if ((w + 4 * i) * 32 >= k) continue;  // wave-uniform: tile past k
+        if ((tb + w + 4 * i) * 32 >= k) continue;  // wave-uniform: tile past k
         if (fast) {
             const int64_t rb = row0 + 4 * h;
             float* gp = a.g_prev + rb * k + kk;
@@ -1864,17 +1873,31 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
     L.split = blocks[0];
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
     if (total == 0) return RT_OK;
-    const dim3 grid(total);
+    // fewer row blocks than half the CUs with two dA tiles per wave (the C1
+    // dz launch at k = 256: 144 row blocks): each row block's dA columns as
+    // two blocks of one tile per wave (RT_DZ_KSPLIT=1/2 forces it, A/B)
+    bool any_da = false;
+    for (int g = 0; g < n_args; ++g) any_da = any_da || args[g].g_prev || args[g].dsrc;
+    static const int ks_env = [] { const char* e = getenv("RT_DZ_KSPLIT"); return e ? atoi(e) : 0; }();
+    unsigned ks = (tpwk == 2 && any_da && total < 128u) ? 2u : 1u;
+    if (ks_env == 1 || (ks_env == 2 && tpwk == 2 && any_da)) ks = static_cast<unsigned>(ks_env);
+    L.ksplit = ks;
+    if (ks == 2) tpwk = 1;
+    const dim3 grid(total * ks);
     hipStream_t st = as_stream(stream);
-#define RT_DZ(T, P)                                                                           \
+#define RT_DZ(T, P, K)                                                                        \
     do {                                                                                      \
-        allow_lds(mlp::linear_bwd_dz_kernel<T, P>, lds);                                      \
-        hipLaunchKernelGGL((mlp::linear_bwd_dz_kernel<T, P>), grid, dim3(256), lds, st, L);   \
+        allow_lds(mlp::linear_bwd_dz_kernel<T, P, K>, lds);                                   \
+        hipLaunchKernelGGL((mlp::linear_bwd_dz_kernel<T, P, K>), grid, dim3(256), lds, st, L); \
     } while (0)
-    switch (tpwk) {
-        case 1: if (wpl) RT_DZ(1, true); else RT_DZ(1, false); break;
-        case 2: if (wpl) RT_DZ(2, true); else RT_DZ(2, false); break;
-        default: RT_DZ(4, false); break;
+    if (ks > 1) {
+        if (wpl) RT_DZ(1, true, true); else RT_DZ(1, false, true);
+    } else {
+        switch (tpwk) {
+            case 1: if (wpl) RT_DZ(1, true, false); else RT_DZ(1, false, false); break;
+            case 2: if (wpl) RT_DZ(2, true, false); else RT_DZ(2, false, false); break;
+            default: RT_DZ(4, false, false); break;
+        }
     }
 #undef RT_DZ
     return check_launch("linear_bwd_dz_kernel");
