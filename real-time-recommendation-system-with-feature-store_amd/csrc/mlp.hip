@@ -1873,13 +1873,13 @@ extern "C" int rt_linear_bwd_dz_f32_multi(const rt_linear_bwd_args* args, int n_
     L.split = blocks[0];
     const unsigned total = blocks[0] + (n_args > 1 ? blocks[1] : 0u);
     if (total == 0) return RT_OK;
-    // fewer row blocks than half the CUs with two dA tiles per wave (the C1
+    // at most one row block per CU with two dA tiles per wave (the C1
     // dz launch at k = 256: 144 row blocks): each row block's dA columns as
     // two blocks of one tile per wave (RT_DZ_KSPLIT=1/2 forces it, A/B)
     bool any_da = false;
     for (int g = 0; g < n_args; ++g) any_da = any_da || args[g].g_prev || args[g].dsrc;
     static const int ks_env = [] { const char* e = getenv("RT_DZ_KSPLIT"); return e ? atoi(e) : 0; }();
-    unsigned ks = (tpwk == 2 && any_da && total < 128u) ? 2u : 1u;
+    unsigned ks = (tpwk == 2 && any_da && total <= 256u) ? 2u : 1u;
     if (ks_env == 1 || (ks_env == 2 && tpwk == 2 && any_da)) ks = static_cast<unsigned>(ks_env);
     L.ksplit = ks;
     if (ks == 2) tpwk = 1;
