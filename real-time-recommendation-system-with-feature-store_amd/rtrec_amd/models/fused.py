@@ -237,7 +237,11 @@ FINALIZE_BN_IN_PRODUCER = os.environ.get("RTREC_BN_FINAL", "0") == "1"
 # 16-byte piece loads per k-block cost more than two float4 loads plus the split
 # — C2 step 0.2428 -> 0.2563 ms in a same-box A/B (profiles/r06_c2_ab_wplanes.txt).
 # RTREC_W_PLANES=1 turns it on.
-SPLIT_W_PLANES = os.environ.get("RTREC_W_PLANES", "0") == "1"
+# RTREC_W_PLANES=fwd / =dz enable one side only (A/B).
+_WPL = os.environ.get("RTREC_W_PLANES", "0")
+SPLIT_W_PLANES = _WPL in ("1", "fwd", "dz")
+SPLIT_W_PLANES_FWD = _WPL in ("1", "fwd")
+SPLIT_W_PLANES_DZ = _WPL in ("1", "dz")
 
 
 def stats_arena_size(blocks: List[Block], n_seg: int = 1) -> int:
@@ -404,7 +408,7 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         # SPLIT_W_PLANES the forward writes Wᵀ's split pieces instead (n % 8 == 0).
         wt = wtp = None
         if li > 0 and lin.training:
-            if SPLIT_W_PLANES and lin.out_features % 8 == 0:
+            if SPLIT_W_PLANES and SPLIT_W_PLANES_DZ and lin.out_features % 8 == 0:
                 wtp = torch.empty((3, lin.in_features, lin.out_features), dtype=torch.int16, device=dev)
                 a.wt_planes_out = wtp.data_ptr()
             else:
@@ -415,7 +419,7 @@ def _forward_plan(blocks: List[Block], src: torch.Tensor, ids: Optional[torch.Te
         # W's split pieces for this launch's k-loop, written by the previous
         # launch of the chain (layers past the first; k % 8 == 0, n <= 128)
         wp = None
-        if SPLIT_W_PLANES and li > 0 and lin.in_features % 8 == 0 and lin.out_features <= 128:
+        if SPLIT_W_PLANES and SPLIT_W_PLANES_FWD and li > 0 and lin.in_features % 8 == 0 and lin.out_features <= 128:
             wp = torch.empty((3, lin.out_features, lin.in_features), dtype=torch.int16, device=dev)
             prev = layers[li - 1]
             prev.next_w = lin.weight.data_ptr()

@@ -23,9 +23,10 @@ def _model(device, dropout=0.2):
 
 @pytest.fixture
 def planes_switch():
-    keep = fused.SPLIT_W_PLANES
+    keep = (fused.SPLIT_W_PLANES, fused.SPLIT_W_PLANES_FWD, fused.SPLIT_W_PLANES_DZ)
+    fused.SPLIT_W_PLANES_FWD = fused.SPLIT_W_PLANES_DZ = True
     yield
-    fused.SPLIT_W_PLANES = keep
+    fused.SPLIT_W_PLANES, fused.SPLIT_W_PLANES_FWD, fused.SPLIT_W_PLANES_DZ = keep
 
 
 def test_tower_forward_bit_identical_with_planes(device, planes_switch):
