@@ -392,8 +392,10 @@ def _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform, 
     if world == 1:
         all_ids = ids
         rows = gather_fn(table_shard, all_ids, row_begin)
-        loc = all_ids - int(row_begin)
-        owned = ((loc >= 0) & (loc < table_shard.shape[0])).sum().reshape(1)
+
+        def owned():  # computed only when a caller tracks the id range (no kernels otherwise)
+            loc = all_ids - int(row_begin)
+            return ((loc >= 0) & (loc < table_shard.shape[0])).sum().reshape(1)
         return rows, all_ids, owned, n_valid, rec
     # ids (padded to the batch width with -1) and the rank's row window in ONE all-gather
     send = torch.full((width + 2,), -1, dtype=torch.int64, device=dev)
@@ -456,9 +458,14 @@ def _gather_global(table_shard, row_begin, ids, group, gather, counts, uniform, 
     return rows, all_ids, owned, n_valid, rec
 
 
-def _status_update(status: Optional[torch.Tensor], check: bool, n_valid: int, owned_total: torch.Tensor):
+def _status_update(status: Optional[torch.Tensor], check: bool, n_valid: int, owned_total):
     """(positions, positions owned by some rank) added to ``status``; they
-    differ iff some id lies outside every window. ``check`` reads them (sync)."""
+    differ iff some id lies outside every window. ``check`` reads them (sync).
+    ``owned_total``: int64 [1] on the device, or a callable returning it."""
+    if status is None and not check:
+        return
+    if callable(owned_total):
+        owned_total = owned_total()
     st = torch.cat([torch.full((1,), n_valid, dtype=torch.int64, device=owned_total.device),
                     owned_total.reshape(1).to(torch.int64)])
     if status is not None:
@@ -635,6 +642,12 @@ def sharded_inbatch_step(table_shard: torch.Tensor, row_begin: int, user_emb: to
     loss_fn = loss_fn or (lambda u, p, off: kernels.inbatch_loss(u, p, temperature, label_offset=off))
     loss, du, dp = loss_fn(user_emb, rows, rank * b)
     lv = loss[0:1]
+    if world == 1:  # the same results with no rescaling kernels (a mean over one rank)
+        if status is not None:
+            _status_update(status, False, n_valid, owned)
+        if grad_shard is not None:
+            sharded_scatter_add_rows(grad_shard, row_begin, gids, dp.float(), group, scatter_add)
+        return lv, du, dp
     if world > 1:
         lv = lv.to(torch.float64, copy=True)
         dist.all_reduce(lv, op=dist.ReduceOp.SUM, group=group)
