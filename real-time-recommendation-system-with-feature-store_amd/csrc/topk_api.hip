@@ -147,12 +147,16 @@ inline double log_binom_tail(int n, double f, int r) {
 }
 
 // the v4 sample: the sparsest stride whose smallest safe rank keeps the expected
-// candidates per (split, query) near rank/f <= ~360. "Safe": the estimate
-// overshoots the split's k-th score (a rescan) with probability <= 1e-6 —
-// P(>= rank of the split's top k fall in the sample) for a 1/f sample; the
+// candidates per query, rank/f, within RT_TOPK_V4_APPEND_CAP. "Safe": the
+// estimate overshoots the split's k-th score (a rescan) with probability <= 1e-6
+// — P(>= rank of the split's top k fall in the sample) for a 1/f sample; the
 // group-maximum estimate sits at or below the item rank, so this bounds it.
+// Cap 500 (round 6; 960 before): k = 100 at the C4 shard and the 1M corpus
+// takes stride 32 / rank 15 (~460 appends) instead of 64 / 11 (~670): the
+// twice denser sample costs less than the appends and finish input it saves,
+// 3-7 % at 125K and 2 % at 1M (profiles/r06_topk_stride_sweep.txt).
 #ifndef RT_TOPK_V4_APPEND_CAP
-#define RT_TOPK_V4_APPEND_CAP 960.0
+#define RT_TOPK_V4_APPEND_CAP 500.0
 #endif
 #ifndef RT_TOPK_V4_MAX_STRIDE
 #define RT_TOPK_V4_MAX_STRIDE 64

@@ -23,7 +23,7 @@
 //      * main phase: every stage (the sample stages again), each score >= thr
 //        appended to the query's candidate buffer (per lane half: one
 //        SADDR 8-byte store at the lane's cursor). About rank / f appends
-//        per query (~600 at the C4 shapes), against thousands for a running
+//        per query (~460 at the C4 shapes), against thousands for a running
 //        threshold that starts at -inf. A half nearing its capacity is
 //        compacted by the v2 radix compaction (threshold raised, never lowered).
 //        The filter of a set is a branch-free 16-bit pass mask (two VALU per

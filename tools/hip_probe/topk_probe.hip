@@ -37,7 +37,8 @@ static void fill(std::vector<__half>& v, int64_t n, int d, uint64_t seed) {
 int main(int argc, char** argv) {
     const int64_t nq = argc > 1 ? atoll(argv[1]) : 65536, nx = argc > 2 ? atoll(argv[2]) : 125000;
     const int v4mode = argc > 3 ? atoi(argv[3]) : 0;  // rt_flatip_topk_tuning mode (0 auto, 1 old, 2 v4)
-    rt_flatip_topk_tuning(v4mode, 0, -1);
+    // optional planner overrides: sample stride and rank (argv 4, 5)
+    rt_flatip_topk_tuning(v4mode, argc > 4 ? atoi(argv[4]) : 0, argc > 5 ? atoi(argv[5]) : -1);
     const int d = 128, reps = 3;
     std::vector<__half> hq(nq * d), hx(nx * d);
     fill(hq, nq, d, 1);
