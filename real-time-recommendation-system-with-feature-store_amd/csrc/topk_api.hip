@@ -1,7 +1,11 @@
 // C ABI for the Flat-IP top-K (rt_flatip_topk) and the candidate-list merge
 // (rt_topk_merge, used for split corpora and for the multi-GPU merge of
 // per-shard top-K lists after an RCCL all-gather).
+#include <array>
 #include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "topk_impl.h"
 
@@ -126,24 +130,27 @@ static int g_v4_joint = 1;    // 1: over several splits, one corpus-wide thresho
 static int g_dense = 1;       // 1: fp32 small corpora take the GEMM + select pair (topk_dense.h)
 static int g_v4_presample = 1;  // 1: joint thresholds from one sample-only launch over every split
 
-// log P(Bin(n, f) >= r)
-inline double log_binom_tail(int n, double f, int r) {
-    if (r <= 0) return 0.0;
-    if (r > n) return -1e300;
-    double acc = 0.0;
-    bool any = false;
-    double mx = -1e300;
-    double terms[kMaxK + 1];
-    for (int i = r; i <= n; ++i) {
-        const double t = std::lgamma(n + 1.0) - std::lgamma(i + 1.0) - std::lgamma(n - i + 1.0) + i * std::log(f) +
-                         (n - i) * std::log1p(-f);
-        terms[i] = t;
-        if (t > mx) mx = t;
-        any = true;
-    }
-    if (!any) return -1e300;
-    for (int i = r; i <= n; ++i) acc += std::exp(terms[i] - mx);
-    return mx + std::log(acc);
+// Smallest failure-safe rank: the least r in [1, r_max] with P(Bin(n, f) >= r)
+// <= 1e-6 (r > n: probability 0, safe), 0 when none. The binomial tail of
+// every r comes from one pass over the pmf (n <= kMaxK terms), summed from the
+// top — the planner below evaluates it for up to 63 strides per plan, on the
+// host path of every search call (a log-sum-exp tail per (stride, rank) pair
+// cost ~1.7 ms per call at the C4 shapes).
+inline int safe_rank(int n, double f, int r_max) {
+    static const auto lf = [] {  // log i!
+        std::array<double, kMaxK + 2> t{};
+        for (int i = 0; i <= kMaxK + 1; ++i) t[i] = std::lgamma(i + 1.0);
+        return t;
+    }();
+    if (n < 0 || n > kMaxK || !(f > 0.0)) return 0;
+    if (f >= 1.0) return n + 1 <= r_max ? n + 1 : 0;  // X = n: only r > n is safe
+    double tail[kMaxK + 2];
+    tail[n + 1] = 0.0;
+    const double lf_ = std::log(f), lg = std::log1p(-f);
+    for (int i = n; i >= 0; --i) tail[i] = tail[i + 1] + std::exp(lf[n] - lf[i] - lf[n - i] + i * lf_ + (n - i) * lg);
+    for (int r = 1; r <= r_max; ++r)
+        if (r > n || tail[r] <= 1e-6) return r;
+    return 0;
 }
 
 // the v4 sample: the sparsest stride whose smallest safe rank keeps the expected
@@ -172,12 +179,8 @@ inline void plan_v4_sample(int k, int64_t items_per_split, int& stride, int& ran
         const int64_t nsa = (nst + st - 1) / st;
         if (nsa < 4) continue;  // fewer than 32 groups per query in the sample
         const double f = static_cast<double>(nsa) / static_cast<double>(nst);
-        for (int r = 1; r <= 2 * v4::kList; ++r) {
-            if (log_binom_tail(k, f, r) <= std::log(1e-6)) {
-                if (r / f <= RT_TOPK_V4_APPEND_CAP) { stride = st; rank = r; return; }
-                break;
-            }
-        }
+        const int r = safe_rank(k, f, 2 * v4::kList);
+        if (r > 0 && r / f <= RT_TOPK_V4_APPEND_CAP) { stride = st; rank = r; return; }
     }
 }
 
@@ -195,13 +198,31 @@ inline void plan_v4_sample_split(int k, int64_t nx, int64_t items_per_split, int
         const int64_t nsa = nfull * ((sps + st - 1) / st) + (rem + st - 1) / st;
         if (nsa < 4) continue;
         const double f = static_cast<double>(nsa) / static_cast<double>(nst);
-        for (int r = 1; r <= 2 * v4::kList; ++r) {
-            if (log_binom_tail(k, f, r) <= std::log(1e-6)) {
-                if (r / f <= RT_TOPK_V4_APPEND_CAP) { stride = st; rank = r; return; }
-                break;
-            }
+        const int r = safe_rank(k, f, 2 * v4::kList);
+        if (r > 0 && r / f <= RT_TOPK_V4_APPEND_CAP) { stride = st; rank = r; return; }
+    }
+}
+
+// (stride, rank) per (kind, k, rows, rows per split), computed once per shape
+inline void plan_v4_sample_cached(bool split_form, int k, int64_t nx, int64_t items_per_split, int& stride,
+                                  int& rank) {
+    static std::mutex mu;
+    static std::map<std::tuple<bool, int, int64_t, int64_t>, std::pair<int, int>> memo;
+    const auto key = std::make_tuple(split_form, k, nx, items_per_split);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        const auto it = memo.find(key);
+        if (it != memo.end()) {
+            stride = it->second.first;
+            rank = it->second.second;
+            return;
         }
     }
+    if (split_form) plan_v4_sample_split(k, nx, items_per_split, stride, rank);
+    else plan_v4_sample(k, items_per_split, stride, rank);
+    std::lock_guard<std::mutex> g(mu);
+    if (memo.size() > 4096) memo.clear();
+    memo[key] = {stride, rank};
 }
 
 // v4 (sampled-threshold scan + finish) for 16-bit, d <= 128, 32 < k <= 128 over
@@ -234,8 +255,8 @@ inline bool plan_v4(int64_t nq, int64_t nx, int d, int dtype, int k, Plan& p) {
     // splits times that); one split: the per-split form
     p.v4_joint = (p.splits > 1 && g_v4_joint) ? 1 : 0;
     p.v4_presample = (p.v4_joint && g_v4_presample) ? 1 : 0;
-    if (p.v4_presample) plan_v4_sample_split(k, nx, p.items_per_split, p.stride, p.rank);
-    else plan_v4_sample(k, p.v4_joint ? nx : p.items_per_split, p.stride, p.rank);
+    if (p.v4_presample) plan_v4_sample_cached(true, k, nx, p.items_per_split, p.stride, p.rank);
+    else plan_v4_sample_cached(false, k, 0, p.v4_joint ? nx : p.items_per_split, p.stride, p.rank);
     if (p.v4_presample && (p.stride <= 0 || p.rank <= 0)) p.v4_presample = 0;  // no sample fits: round-4 form
     if (g_v4_stride > 0) p.stride = g_v4_stride;
     if (g_v4_rank >= 0) p.rank = g_v4_rank;
@@ -485,9 +506,8 @@ extern "C" int rt_flatip_topk_shard_sample(const void* queries, int64_t nq, cons
 extern "C" int rt_topk_sample_rank(int k, int64_t sampled_stages, int64_t stages, int* rank) {
     if (k <= 0 || k > topk::v4::kMaxK || sampled_stages <= 0 || stages < sampled_stages || !rank) return RT_ERR_INVALID;
     const double f = static_cast<double>(sampled_stages) / static_cast<double>(stages);
-    *rank = 0;  // 0: no failure-safe rank within the lists (the caller scans from -inf)
-    for (int r = 1; r <= topk::v4::kSampleList; ++r)
-        if (topk::log_binom_tail(k, f, r) <= std::log(1e-6)) { *rank = r; break; }
+    // 0: no failure-safe rank within the lists (the caller scans from -inf)
+    *rank = topk::safe_rank(k, f, topk::v4::kSampleList);
     return RT_OK;
 }
 

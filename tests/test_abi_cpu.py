@@ -123,3 +123,36 @@ def test_ctypes_argument_counts_match_header(native):
         params = params.strip()
         n = 0 if params in ("", "void") else params.count(",") + 1
         assert len(native.SIGNATURES[name][1]) == n, (name, n, len(native.SIGNATURES[name][1]))
+
+
+def test_sample_rank_matches_binomial_tail(native):
+    """rt_topk_sample_rank (host-only) is the least rank r <= 32 with
+    P(Bin(k, f) >= r) <= 1e-6 for f = sampled / stages (r > k: safe; 0 when
+    none fits) — the failure bound of the v4 sampled threshold
+    (topk_api.hip::safe_rank), checked against scipy's binomial tail."""
+    from scipy.stats import binom
+    L = native.lib()
+    for k in (1, 10, 33, 64, 100, 128):
+        for stages in (64, 977, 7813):
+            for sampled in sorted(x for x in {1, 4, 16, 31, 62, 124, stages // 2, stages} if x <= stages):
+                r = ctypes.c_int(-1)
+                assert L.rt_topk_sample_rank(k, sampled, stages, ctypes.byref(r)) == 0
+                f = sampled / stages
+                want = next((rr for rr in range(1, 33) if rr > k or binom.sf(rr - 1, k, f) <= 1e-6), 0)
+                assert r.value == want, (k, sampled, stages, r.value, want)
+
+
+def test_shard_plan_is_cheap_on_the_host(native):
+    """The v4 plan runs on the host path of every search call: after the first
+    call of a shape its (stride, rank) come from a memo (a per-(stride, rank)
+    log-sum-exp tail once cost ~1.7 ms per call)."""
+    import time
+    L = native.lib()
+    counts = (ctypes.c_int64 * 2)()
+    args = (ctypes.c_int64(65536), ctypes.c_int64(125000), 128, 1, 100, 64, ctypes.cast(counts, ctypes.c_void_p))
+    assert L.rt_flatip_topk_shard_plan(*args) == 0
+    assert list(counts) == [16, 977]
+    t0 = time.perf_counter()
+    for _ in range(200):
+        L.rt_flatip_topk_shard_plan(*args)
+    assert (time.perf_counter() - t0) / 200 < 2e-4
