@@ -8,8 +8,10 @@
 // 1. flatip_topk_v4_scan: block = 8 waves x QS sets of 32 queries (QS = 2:
 //    64 queries per wave, 512 per block; every A fragment read from LDS feeds
 //    two MFMAs, and a block's item stream serves 512 queries), over one item
-//    split. Rows stream through the three-stage LDS ring of the v3 scan
-//    (SADDR LDS-DMA, one pad chunk per row, immediate-offset A fragments).
+//    split. Rows stream through an LDS ring as in the v3 scan (SADDR
+//    LDS-DMA, one pad chunk per row, immediate-offset A fragments): three
+//    stages with a barrier inside each, or at d = 128 four stages with a
+//    barrier after every other one (see main_pass).
 //    Selection runs against a SAMPLED threshold instead of a running one:
 //      * sample phase: every `stride`-th stage of the split (a 1/stride
 //        sample). Per lane and query set the 16 largest group maxima
@@ -95,7 +97,11 @@ struct Cfg4 {
     static constexpr int PIECES = SLOTS / 64;      // 1 KiB DMA pieces per stage
     static constexpr int MAXP = (PIECES + kWavesB - 1) / kWavesB;
     static constexpr int TILE_BYTES = SLOTS * 16;
+#ifdef RT_TOPK_V4_RING3  // A/B: a block barrier inside every stage at d = 128 too
     static constexpr int RING = 3;
+#else
+    static constexpr int RING = S == 8 ? 4 : 3;    // d = 128: a block barrier every other stage
+#endif
     static constexpr int HIST_BYTES = kWavesB * 1024;
     static constexpr int LDS_BYTES = RING * TILE_BYTES + HIST_BYTES + 16;
     static_assert(PIECES * 64 == SLOTS, "whole DMA pieces");
@@ -700,10 +706,27 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
     //   can already read its fragments), and every wave is past stage v-1, so
     //   stage v+2 is DMA'd into that buffer right after it. The DMA has one
     //   stage to land.
+    // RING = 4 (d = 128; 4 x 34.8 KB ring): the block barrier sits at the END of every
+    // odd stage v instead of inside every stage. Before it each wave waits for
+    // its pieces of stages v+1 and v+2 (DMA'd two stages earlier); after it,
+    // stages v+3 and v+4 go into the buffers of v-1 and v, and stage v+1's first
+    // fragments are re-read (the prefetch in v's last sub-tile may have read
+    // them before they landed). Waves drift apart by up to two stages between
+    // barriers instead of one sub-tile.
+    constexpr bool R4 = C::RING == 4;
     auto main_pass = [&]() {
         if (nst == 0) return;
         int mk_next;
-        {
+        if constexpr (R4) {
+            fetch(stage_t0(0, false), 0);
+            if (nst > 1) fetch(stage_t0(1, false), 1);
+            const int m01 = issued;
+            if (nst > 2) fetch(stage_t0(2, false), 2);
+            if (nst > 3) fetch(stage_t0(3, false), 3);
+            mk_next = issued;
+            wait_vm_le(issued - m01);
+            raw_barrier();
+        } else {
             fetch(stage_t0(0, false), 0);
             const int mark0 = issued;
             if (nst > 1) fetch(stage_t0(1, false), 1);
@@ -742,7 +765,7 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
             RT_PT(uint64_t c0 = clock64();)
 #pragma unroll
             for (int rt = 0; rt < C::NSUB; ++rt) {
-                if (rt == C::NSUB - 1) {
+                if (!R4 && rt == C::NSUB - 1) {
                     RT_PT(const uint64_t c1 = clock64(); pc_main += c1 - c0;)
                     if (more) wait_vm_le(issued - mk_next);
                     RT_PT(const uint64_t c2 = clock64(); pc_wait += c2 - c1;)
@@ -804,6 +827,17 @@ __global__ __launch_bounds__(512) void flatip_topk_v4_scan(Args a, int splits, i
                 }
             }
             RT_PT(pc_main += clock64() - c0;)
+            if constexpr (R4) {
+                if (more) maybe_compact();  // wave-local: one stage of appends between checks
+                if (more && (v & 1)) {
+                    wait_vm_le(issued - mk_next);  // this wave's pieces of stages v+1, v+2
+                    raw_barrier();
+                    if (v + 3 < nst) fetch(stage_t0(v + 3, false), (v + 3) & 3);
+                    if (v + 4 < nst) fetch(stage_t0(v + 4, false), v & 3);
+                    mk_next = issued;
+                    lds_a(af, nstage, 0);
+                }
+            }
             cur = cur == C::RING - 1 ? 0 : cur + 1;
         }
         if constexpr (QS > 1) store_loop(QS - 1, passmask(QS - 1, acc[QS - 1], sub_prev, tm_prev), acc[QS - 1], sub_prev);
