@@ -108,4 +108,59 @@ __device__ __forceinline__ void wave_sort_regs(float (&s)[E], uint32_t (&id)[E])
     }
 }
 
+// ---- E = 2, every stage unrolled ---------------------------------------------
+// The 128-entry sort of the v4 finish: lane distances 1 and 2 by DPP quad
+// permutes (no LDS round trip), 4..16 by ds_swizzle in xor mode, 32 by
+// ds_bpermute; each stage's per-lane direction is one compare of two lane bits.
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+    const int x = static_cast<int>(v);
+    if constexpr (M == 1) return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));
+    else if constexpr (M == 2) return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));
+    else if constexpr (M < 32) return static_cast<uint32_t>(__builtin_amdgcn_ds_swizzle(x, 0x1F | (M << 10)));
+    else return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(((threadIdx.x & 63) ^ 32) << 2, x));
+}
+
+// better() without short-circuit branches: three compares, mask logic, selects
+__device__ __forceinline__ bool better_nb(float sa, uint32_t ia, float sb, uint32_t ib) {
+    return (sa > sb) | ((sa == sb) & (ia < ib));
+}
+
+template <int SIZE, int STRIDE>
+__device__ __forceinline__ void sort2_stage(float (&s)[2], uint32_t (&id)[2], int lane) {
+    if constexpr (STRIDE == 1) {  // the lane's own pair (elements 2·lane, 2·lane + 1)
+        const bool dir = ((2 * lane) & SIZE) == 0;
+        const bool sw = better_nb(s[1], id[1], s[0], id[0]) == dir;
+        const float s0 = s[0], s1 = s[1];
+        const uint32_t i0 = id[0], i1 = id[1];
+        s[0] = sw ? s1 : s0;
+        s[1] = sw ? s0 : s1;
+        id[0] = sw ? i1 : i0;
+        id[1] = sw ? i0 : i1;
+    } else {  // partner lane = lane ^ STRIDE / 2
+        constexpr int M = STRIDE / 2;
+        const bool keep_better = ((lane & M) == 0) == ((lane & (SIZE / 2)) == 0);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const float os = __uint_as_float(xor_lane<M>(__float_as_uint(s[j])));
+            const uint32_t oi = xor_lane<M>(id[j]);
+            const bool take = keep_better != better_nb(s[j], id[j], os, oi);
+            s[j] = take ? os : s[j];
+            id[j] = take ? oi : id[j];
+        }
+    }
+}
+
+template <int SIZE, int STRIDE>
+__device__ __forceinline__ void sort2_from(float (&s)[2], uint32_t (&id)[2], int lane) {
+    sort2_stage<SIZE, STRIDE>(s, id, lane);
+    if constexpr (STRIDE > 1) sort2_from<SIZE, STRIDE / 2>(s, id, lane);
+    else if constexpr (SIZE < 128) sort2_from<SIZE * 2, SIZE>(s, id, lane);
+}
+
+// wave_sort_regs<2> with every stage unrolled
+__device__ __forceinline__ void wave_sort_regs2(float (&s)[2], uint32_t (&id)[2]) {
+    sort2_from<2, 1>(s, id, static_cast<int>(threadIdx.x & 63));
+}
+
 }  // namespace rt

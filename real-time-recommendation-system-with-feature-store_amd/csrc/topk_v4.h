@@ -908,7 +908,11 @@ __device__ __noinline__ void finish_sort(const Cand* __restrict__ buf, int m, in
         s[j] = c.s;
         id[j] = c.i;
     }
-    wave_sort_regs<E>(s, id);
+#ifndef RT_SORT2_GENERIC  // A/B: the loop form
+    if constexpr (E == 2) wave_sort_regs2(s, id);
+    else
+#endif
+        wave_sort_regs<E>(s, id);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
         const int r = lane * E + j;
