@@ -155,4 +155,4 @@ def test_shard_plan_is_cheap_on_the_host(native):
     t0 = time.perf_counter()
     for _ in range(200):
         L.rt_flatip_topk_shard_plan(*args)
-    assert (time.perf_counter() - t0) / 200 < 2e-4
+    assert (time.perf_counter() - t0) / 200 < 1e-3  # loose: CPU-contended runners
