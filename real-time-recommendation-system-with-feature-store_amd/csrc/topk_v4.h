@@ -189,7 +189,10 @@ __device__ __forceinline__ void radix_prefix(Each&& each, int k, int limit, uint
     const int lane = threadIdx.x & 63;
     int need = k;  // entries still to be found inside the current prefix bucket
     while (shift > 0) {
-        const int sh = shift - 8;
+        // the last pass may have fewer than 8 bits left (the finish starts below
+        // the keys' shared prefix, at any bit): its bins are the low 8 bits, the
+        // ones above `shift` fixed by the prefix
+        const int sh = shift > 8 ? shift - 8 : 0;
         reinterpret_cast<uint4*>(hist)[lane] = make_uint4(0u, 0u, 0u, 0u);
         wave_lds_sync();
         const uint64_t pmask = prefix_mask(shift), pre = prefix;

@@ -388,3 +388,33 @@ def test_flat_l2_save_load_and_errors(K, tmp_path):
         HipFlatIPIndex({"dimension": 64, "metric": "l2", "storage_dtype": "float16"})
     with pytest.raises(ValueError, match="k="):
         idx.search(q, 513)
+
+
+@pytest.mark.parametrize("n_lists,k_in,k_out,dup", [(8, 100, 100, False), (4, 100, 100, False), (3, 37, 50, False),
+                                                    (8, 100, 64, True), (2, 128, 128, True)])
+def test_topk_merge_sorted_lists(K, n_lists, k_in, k_out, dup):
+    """Lists in (score desc, id asc) order with their -1 padding last — the
+    per-shard top-K the multi-GPU owner merge receives — through
+    rt_topk_merge's register select (<= 1,024 candidates into <= 128): score
+    ties across lists, short (padded) lists, k_out below and above k_in, and
+    (dup) the same (score, id) in two lists. Equal to the oracle's full sort."""
+    rng = np.random.default_rng(100 * n_lists + k_in)
+    nq = 700
+    s = np.round(rng.standard_normal((n_lists, nq, k_in)), 1).astype(np.float32)  # many exact ties
+    i = rng.choice(10**6, (n_lists, nq, k_in)).astype(np.int64)
+    for l in range(n_lists):
+        i[l] = i[l] // n_lists * n_lists + l
+    if dup:  # list 1 repeats some entries of list 0
+        i[1, :, :10] = i[0, :, :10]
+        s[1, :, :10] = s[0, :, :10]
+    nvalid = rng.integers(0, k_in + 1, (n_lists, nq))
+    for l in range(n_lists):
+        for q in range(nq):
+            o = np.lexsort((i[l, q], -s[l, q]))  # score desc, id asc
+            s[l, q], i[l, q] = s[l, q][o], i[l, q][o]
+            i[l, q, nvalid[l, q]:] = -1
+            s[l, q, nvalid[l, q]:] = -np.finfo(np.float32).max
+    rs, ri = orc.topk_merge(s, i, k_out)
+    gs, gi = K.topk_merge(torch.from_numpy(s).cuda(), torch.from_numpy(i).cuda(), k_out)
+    assert np.array_equal(gi.cpu().numpy(), ri)
+    assert np.array_equal(gs.cpu().numpy(), rs)
